@@ -1,0 +1,198 @@
+"""Pin the CPU oracle against the committed golden fixtures (CPU only).
+
+The fixtures come from an independent pure-Python transliteration of the
+reference (rules, MCTS, self-play) and from libtorch CPU for the net; see
+tests/golden/gen_golden.py.  No reference outputs exist (no tests, not
+buildable), so these pins are restatement-vs-restatement for rules/search and
+libtorch-anchored for the net.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+
+def _load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def rules_c4():
+    return _load("rules_c4.json")
+
+
+def test_nd_sum_order(oracle):
+    # ndarray unrolled_fold: 9 elements sum as ((x0+x4)+(x1+x5)+(x2+x6)+(x3+x7))+x8
+    x = np.array([1e8, 1, 1, 1, -1e8, 1, 1, 1, 1], np.float32)
+    got = oracle.lib().or_nd_sum(oracle._f(x), 9)
+    p = np.float32(0)
+    for a, b in [(0, 4), (1, 5), (2, 6), (3, 7)]:
+        p = np.float32(p + np.float32(x[a] + x[b]))
+    assert got == np.float32(p + x[8])
+
+
+def test_c4_rules_traces(oracle, rules_c4):
+    rng = np.random.default_rng(0)
+    for g in rules_c4["traces"]:
+        s = oracle.C4()
+        plies = g["plies"]
+        for i, p in enumerate(plies):
+            assert s.legal_mask() == p["legal"]
+            assert s.status == p["status"] and s.n == p["n"] and s.current_player == p["cur"]
+            x, o = s.bitboards()
+            assert (str(x), str(o)) == (p["x"], p["o"])
+            v, t = s.value_terminated()
+            assert (v, t) == (p["value"], p["term"])
+            enc = s.encoding()
+            assert float(enc.ravel() @ np.arange(enc.size)) == p["enc_sum"]
+            if i + 1 < len(plies):
+                # find the move that produced the next ply from the bitboards
+                nx = int(plies[i + 1]["x"]) | int(plies[i + 1]["o"])
+                diff = nx ^ (x | o)
+                col = (diff.bit_length() - 1) // 7
+                s = s.next_state(col)
+
+
+def test_c4_kats(oracle, rules_c4):
+    for k in rules_c4["kats"]:
+        s = oracle.C4()
+        for a in k["moves"]:
+            s = s.next_state(a)
+        if "illegal" in k:
+            with pytest.raises(ValueError):
+                s.next_state(k["illegal"])
+            assert s.legal_mask() == k["legal"]
+        else:
+            assert s.status == k["status"], k["name"]
+            assert s.n == k["n"]
+    # quirk Q1 explicitly: the anti-diagonal four stays Ongoing
+    kat = [k for k in rules_c4["kats"] if k["name"] == "anti_diagonal_ignored"][0]
+    assert kat["status"] == oracle.ONGOING
+
+
+def test_c4_game_over_errors(oracle):
+    s = oracle.C4()
+    for a in [0, 1, 0, 1, 0, 1, 0]:
+        s = s.next_state(a)
+    assert s.status == oracle.WON and s.valid_actions() == []
+    with pytest.raises(ValueError):
+        s.next_state(2)
+
+
+def test_c4_mask_invalid(oracle):
+    s = oracle.C4()
+    for a in [0] * 6:
+        s = s.next_state(a)
+    p = np.array([0.3, 0.1, 0.1, 0.1, 0.1, 0.1, 0.2], np.float32)
+    m = s.mask_invalid(p)
+    assert m[0] == 0.0
+    mp = p * np.array([0, 1, 1, 1, 1, 1, 1], np.float32)
+    ssum = np.float32(0)
+    for v in mp:
+        ssum = np.float32(ssum + v)
+    np.testing.assert_array_equal(m, mp / ssum)
+    with pytest.raises(ValueError):
+        s.mask_invalid(np.ones(6, np.float32))
+
+
+def test_ttt_traces(oracle):
+    d = _load("rules_ttt.json")
+    for g in d["traces"]:
+        s = oracle.TTT()
+        plies = g["plies"]
+        for i, p in enumerate(plies):
+            assert s.status == p["status"]
+            if i + 1 < len(plies):
+                nx = int(plies[i + 1]["x"]) | int(plies[i + 1]["o"])
+                cur = int(p["x"]) | int(p["o"])
+                a = (nx ^ cur).bit_length() - 1
+                s = s.next_state(a)
+
+
+def test_sampler_matches_python(oracle):
+    # Philox uniform + weighted index vs the Python transliteration in gen_golden
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gg", os.path.join(GOLDEN, "gen_golden.py"))
+    gg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gg)
+    L = oracle.lib()
+    for seed, gid, mv in [(0, 0, 0), (7, 3, 11), (2**40 + 5, 123456, 2**33 + 1)]:
+        assert L.or_uniform(seed, gid, mv) == gg.uniform(seed, gid, mv)
+    vis = np.array([3, 0, 10, 1, 7], np.float32)
+    for u in [0.0, 0.1, 0.5, 0.77, 0.999999]:
+        assert L.or_weighted_index(oracle._f(vis), 5, np.float32(1.25), u) == gg.weighted_index(vis, 1.25, u)
+
+
+def test_mcts_search_hash(oracle):
+    d = _load("mcts_hash.json")
+    assert d["search"], "fixture has no cases"
+    for case in d["search"]:
+        # rebuild the root from bitboards by replaying stones (order does not matter for the tree)
+        x, o = int(case["x"]), int(case["o"])
+        s = _c4_from_bitboards(oracle, x, o)
+        assert s.n == case["n"]
+        rc, pol, ids, vis, nc = oracle.search_c4([s], case["sims"])
+        k = nc[0]
+        assert [int(v) for v in vis[0, :k]] == case["visits"]
+        exp = np.array(case["policy"], np.float32)
+        np.testing.assert_array_equal(pol[0], exp)
+
+
+def test_mcts_uniform_first_select(oracle):
+    # ties go to the LAST child (mcts.rs:110-113) -> column 6
+    d = _load("mcts_hash.json")
+    assert d["uniform_first_select"] == 6
+    rc, pol, ids, vis, nc = oracle.search_c4([oracle.C4()], 2, eval_kind=oracle.EVAL_UNIFORM)
+    assert list(vis[0, :nc[0]]) == [0, 0, 0, 0, 0, 0, 1]
+
+
+@pytest.mark.parametrize("game", ["c4", "ttt"])
+def test_self_play_hash(oracle, game):
+    d = _load("mcts_hash.json")["selfplay"][game]
+    g = oracle.GAME_CONNECT4 if game == "c4" else oracle.GAME_TICTACTOE
+    r = oracle.self_play(g, d["n_games"], d["sims"], d["seed"], eval_kind=oracle.EVAL_HASH)
+    exp = d["samples"]
+    assert len(r["value"]) == len(exp)
+    for i, e in enumerate(exp):
+        assert (int(r["game"][i]), int(r["ply"][i])) == (e["game"], e["ply"])
+        assert float(r["value"][i]) == e["value"]
+        np.testing.assert_array_equal(r["policy"][i], np.array(e["policy"], np.float32))
+        assert float(r["enc"][i] @ np.arange(r["enc"].shape[1])) == e["enc_sum"]
+    for gi, mv in enumerate(d["moves"]):
+        assert list(r["moves"][gi, :r["n_moves"][gi]]) == mv
+
+
+@pytest.mark.parametrize("name,game", [("net_c4_2x64.npz", 1), ("net_ttt_2x64.npz", 0)])
+def test_net_forward_vs_libtorch(oracle, name, game):
+    z = np.load(os.path.join(GOLDEN, name))
+    blocks, hidden, seed = [int(v) for v in z["meta"]]
+    p = oracle.init_params(game, blocks, hidden, seed)
+    np.testing.assert_array_equal(p, z["params"])  # init restatement is bitwise
+    net = oracle.Net(game, blocks, hidden, p)
+    lg, v = net.forward(z["x"])
+    # fp32 vs libtorch fp32 (different summation order): tight tolerance
+    np.testing.assert_allclose(lg, z["logits"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(v, z["value"], rtol=1e-4, atol=1e-5)
+
+
+def _c4_from_bitboards(oracle, x, o):
+    st = oracle.C4State()
+    oracle.lib().or_c4_init(oracle.C.byref(st))
+    n = 0
+    for col in range(7):
+        for row in range(6):
+            b = 1 << (col * 7 + row)
+            if x & b:
+                st.board[row][col] = oracle.X
+                n += 1
+            elif o & b:
+                st.board[row][col] = oracle.O
+                n += 1
+    st.num_actions_played = n
+    st.current_player = oracle.X if n % 2 == 0 else oracle.O
+    return oracle.C4(st)
