@@ -1,0 +1,187 @@
+/*
+ * spai.h — C ABI of the MI355X-native batched self-play MCTS engine.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (joshua16266261/self-play-ai).  The reference is in-process Rust with no FFI;
+ * each entry point below replaces one trait method or function of that path,
+ * cited as path:line relative to the reference root.  A Rust binding that
+ * implements the reference traits on top of these symbols is in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Every function returns SPAI_OK (0) or a negative spai_error.  The message
+ *    of the last failure on the calling thread is spai_last_error().  The
+ *    reference reports rules errors as Result<_, String> (game/mod.rs:26,31)
+ *    and panics on everything else (unwrap); those panics map to error codes.
+ *  - Handles are opaque.  Buffers passed in or out are caller-owned HOST
+ *    memory unless a parameter says "device".  Device memory and HIP streams
+ *    are owned by the engine.
+ *  - No global mutable state: one engine per host thread is fully independent,
+ *    mirroring one Mcts + Model per self-play worker (main.rs:169-186).  An
+ *    engine handle must not be used from two threads at once.
+ *  - Connect4 states cross the boundary as spai_c4_state bitboards:
+ *    bit (col*7 + row) of `x` / `o` holds X's / O's stone, row 0 = bottom
+ *    (connect_four.rs:18), bit 6 of every column is always clear.  X moves
+ *    first; the player to move is X iff num_actions_played is even
+ *    (connect_four.rs:20-26,197).
+ */
+#ifndef SPAI_H
+#define SPAI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPAI_VERSION_MAJOR 0
+#define SPAI_VERSION_MINOR 1
+
+typedef enum spai_error {
+    SPAI_OK = 0,
+    SPAI_ERR_INVALID = -1,       /* bad argument / handle / shape (e.g. mask_invalid_actions length) */
+    SPAI_ERR_ILLEGAL_MOVE = -2,  /* Err("Illegal move: column already filled"), connect_four.rs:193 */
+    SPAI_ERR_GAME_OVER = -3,     /* Err("Game has already ended"), connect_four.rs:209 */
+    SPAI_ERR_DEVICE = -4,        /* HIP runtime failure */
+    SPAI_ERR_NAN = -5,           /* NaN UCB or all-zero visits: the reference panics (mcts.rs:106-109) */
+    SPAI_ERR_CAPACITY = -6,      /* node arena / batch capacity exceeded */
+    SPAI_ERR_UNSUPPORTED = -7    /* game or net shape not built for this device path */
+} spai_error;
+
+typedef enum spai_game { SPAI_GAME_TICTACTOE = 0, SPAI_GAME_CONNECT4 = 1, SPAI_GAME_CHESS = 2 } spai_game;
+typedef enum spai_status { SPAI_ONGOING = 0, SPAI_TIED = 1, SPAI_WON = 2 } spai_status; /* game/mod.rs:9-15 */
+
+/* Evaluator used by search.  NET is Model::predict (model/mod.rs:36-98).  UNIFORM
+ * and HASH are deterministic stub evaluators (not in the reference) used to pin
+ * search and self-play bit-exactly against the CPU oracle. */
+typedef enum spai_eval { SPAI_EVAL_NET = 0, SPAI_EVAL_UNIFORM = 1, SPAI_EVAL_HASH = 2 } spai_eval;
+
+typedef struct spai_c4_state {
+    uint64_t x;                  /* X stones, bit col*7+row */
+    uint64_t o;                  /* O stones */
+    uint8_t num_actions_played;  /* connect_four.rs:24 */
+    uint8_t status;              /* spai_status, connect_four.rs:25 */
+    uint8_t pad[6];
+} spai_c4_state;
+
+/* mcts::Args (mcts.rs:9-18,46-59) + SelfPlayArgs (learner_concurrent.rs:21-26,50-59),
+ * reduced to what the hot path reads, plus device sizing. */
+typedef struct spai_config {
+    float c;                 /* PUCT constant; the reference always uses Args::default().c = 2.0 (quirk Q6) */
+    uint32_t num_searches;   /* simulations per move (Args.num_searches) */
+    float temperature;       /* move sampling exponent on visit counts (learner_concurrent.rs:189-190) */
+    uint32_t max_trees;      /* trees (parallel games) held on the device */
+    uint32_t max_moves;      /* longest game; sizes the node arena (C4: 42) */
+    uint32_t eval;           /* spai_eval */
+    uint64_t seed;           /* move-sampling stream: Philox(seed, game id, move number) */
+} spai_config;
+
+typedef struct spai_engine spai_engine;
+typedef struct spai_net spai_net;
+
+/* ------------------------------------------------------------------ general */
+const char *spai_last_error(void);
+const char *spai_version(void);
+int spai_device_count(int *count);
+int spai_config_default(int game, spai_config *cfg);
+int spai_engine_create(int game, const spai_config *cfg, int device, spai_engine **out);
+int spai_engine_destroy(spai_engine *eng);
+int spai_engine_sync(spai_engine *eng);
+
+/* ------------------------------------------------------------------ rules
+ * The State trait (game/mod.rs:21-33) batched over n engine-held game slots
+ * [first, first+n) laid out as struct-of-arrays bitboards in HBM. */
+int spai_games_resize(spai_engine *eng, uint32_t n);                       /* n slots = State::default() */
+int spai_games_reset(spai_engine *eng, uint32_t first, uint32_t n);
+int spai_games_write(spai_engine *eng, uint32_t first, uint32_t n, const spai_c4_state *states);
+int spai_games_read(spai_engine *eng, uint32_t first, uint32_t n, spai_c4_state *states);
+/* get_valid_actions (connect_four.rs:213-225) as a bitmask: bit a = action a legal */
+int spai_legal_mask(spai_engine *eng, uint32_t first, uint32_t n, uint32_t *mask);
+/* get_next_state (connect_four.rs:190-211) in place; rc[i] = 0 or a spai_error for slot i
+ * (slot left unchanged on error).  Returns SPAI_OK if every slot succeeded, else the first error. */
+int spai_apply(spai_engine *eng, uint32_t first, uint32_t n, const int32_t *actions, int32_t *rc);
+/* get_value_and_terminated (connect_four.rs:231-240) */
+int spai_value_terminated(spai_engine *eng, uint32_t first, uint32_t n, float *value, uint8_t *terminated);
+/* get_encoding (connect_four.rs:242-259): out [n][3][6][7] f32 */
+int spai_encode(spai_engine *eng, uint32_t first, uint32_t n, float *out);
+/* mask_invalid_actions (connect_four.rs:261-279): policy [n][len] -> out [n][7]; len must be 7 */
+int spai_mask_invalid(spai_engine *eng, uint32_t first, uint32_t n, const float *policy, uint32_t len,
+                      float *out);
+/* Device-resident timing of the rules kernels on n random reachable positions:
+ * ms[0] legal mask, ms[1] apply+terminal, ms[2] encode (bf16), per launch. */
+int spai_rules_bench(spai_engine *eng, uint32_t n, uint32_t iters, double *ms);
+
+/* ------------------------------------------------------------------ net
+ * Net trait (model/mod.rs:22-28) + Model::predict (model/mod.rs:36-98).
+ * `params` are fp32 in module construction order (torso, policy head, value
+ * head; conv = weight[co][ci][3][3], bias; batch_norm = weight, bias,
+ * running_mean, running_var; linear = weight[out][in], bias) — the order tch
+ * registers them for model/connect_four.rs:34-44.  Device path: hidden = 64. */
+int spai_net_num_params(int game, int blocks, int hidden, size_t *count);
+int spai_net_init_params(int game, int blocks, int hidden, uint64_t seed, float *params);
+int spai_net_create(spai_engine *eng, int blocks, int hidden, const float *params, size_t nparams,
+                    spai_net **out);
+int spai_net_destroy(spai_net *net);
+/* Net::forward(x, train=false): x [n][3][6][7] f32 -> logits [n][7], value [n] (tanh) */
+int spai_net_forward(spai_net *net, uint32_t n, const float *x, float *logits, float *value);
+/* Model::predict: states -> masked softmax priors [n][7] (softmax then mask_invalid_actions), values [n] */
+int spai_predict(spai_net *net, uint32_t n, const spai_c4_state *states, float *priors, float *values);
+/* Evaluator that search uses when cfg.eval == SPAI_EVAL_NET (Mcts.model, mcts.rs:41-44) */
+int spai_engine_set_net(spai_engine *eng, spai_net *net);
+
+/* ------------------------------------------------------------------ search
+ * Tree (mcts.rs:32-39,67-89,161-192) + Mcts::search (mcts.rs:196-332).
+ * Trees live in HBM; node ids are per-tree handles (stable across
+ * use_subtree; they are NOT the reference's BFS re-indexed arena offsets). */
+int spai_trees_create(spai_engine *eng, uint32_t n);                                   /* n x Tree::default() */
+int spai_tree_reset(spai_engine *eng, uint32_t tree, const spai_c4_state *root);       /* with_root_state; NULL = default */
+/* Runs num_searches iterations over trees tree_idx[0..n).  Per tree i (A = 7):
+ *   policy[i*A + a]       normalized root visit counts (Policy::normalize)
+ *   child_ids[i*A + k]    node id of the k-th root child (legal-action order)
+ *   child_visits[i*A + k] its visit count as f32
+ *   n_children[i]
+ * Any output pointer may be NULL. */
+int spai_search(spai_engine *eng, uint32_t n, const uint32_t *tree_idx, uint32_t num_searches, float *policy,
+                uint32_t *child_ids, float *child_visits, uint32_t *n_children);
+/* Tree::use_subtree(child) for a child of the root; the new root keeps N and W (quirk Q4) */
+int spai_tree_use_subtree(spai_engine *eng, uint32_t tree, uint32_t child_id);
+/* arena[node].state for the root or a root child; visits / value_sum of that node (may be NULL) */
+int spai_tree_node(spai_engine *eng, uint32_t tree, uint32_t node_id, spai_c4_state *state, uint32_t *visits,
+                   float *value_sum);
+int spai_tree_size(spai_engine *eng, uint32_t tree, uint32_t *nodes);
+
+/* ------------------------------------------------------------------ self-play
+ * SelfPlayWorker::self_play (learner_concurrent.rs:169-242): n_games trees
+ * from the default state, search every move, sample a root child with
+ * probability proportional to N^temperature, record (root state, visit policy),
+ * and when the sampled child is terminal emit the game's samples with the value
+ * signed per player to move (:211-225).  The sink is called once per finished
+ * game, in the reference's emission order. */
+typedef void (*spai_sample_sink)(void *user, uint32_t game_id, uint32_t n, const float *encodings /* [n][3*6*7] */,
+                                 const float *policies /* [n][7] */, const float *values /* [n] */,
+                                 const int32_t *moves /* [n] action played at each position */);
+typedef struct spai_selfplay_stats {
+    double sims;        /* trees x search iterations */
+    double evals;       /* leaves sent to the evaluator */
+    double games;       /* finished games */
+    double positions;   /* emitted samples */
+    double moves;       /* search calls (plies of the longest game) */
+    double seconds;     /* wall time of the call */
+} spai_selfplay_stats;
+int spai_selfplay_run(spai_engine *eng, uint32_t n_games, uint64_t game_id_base, spai_sample_sink sink, void *user,
+                      spai_selfplay_stats *stats);
+
+/* ------------------------------------------------------------------ profiling
+ * Per-kernel average device time of the last spai_selfplay_run / spai_search
+ * call, measured with HIP events on the engine stream when enabled. */
+int spai_engine_set_timing(spai_engine *eng, int enabled);
+/* ms[0] select, ms[1] evaluate (NN forward), ms[2] expand+backup; launches[3] */
+int spai_engine_timing(spai_engine *eng, double *avg_ms, double *launches);
+/* totals behind spai_engine_timing: summed sampled ms and the work items those
+ * launches covered (trees for select/expand, evaluated leaves for the forward) */
+int spai_engine_timing_items(spai_engine *eng, double *total_ms, double *items);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -57,6 +57,9 @@ def lib():
         L.or_c4_encoding.argtypes = [vp, fp]
         L.or_c4_mask_invalid.argtypes = [vp, fp, i, fp]
         L.or_c4_bitboards.argtypes = [vp, C.POINTER(u64), C.POINTER(u64)]
+        L.or_c4_replay.restype = C.c_long
+        L.or_c4_replay.argtypes = [i, i, i32p, vp, vp, vp, vp, i32p]
+        L.or_encode_states.argtypes = [i, i, C.POINTER(vp), fp]
         L.or_ttt_init.argtypes = [vp]
         L.or_ttt_next_state.argtypes = [vp, i, vp]
         L.or_uniform.restype = d
@@ -178,6 +181,20 @@ class TTT:
     @property
     def status(self):
         return self.st.status
+
+
+def c4_replay(actions):
+    """actions [n][P] int32 (-1 = stop) -> dict of per-ply arrays [n][P+1]"""
+    a = np.ascontiguousarray(actions, np.int32)
+    n, P = a.shape
+    legal = np.zeros((n, P + 1), np.uint32)
+    status = np.zeros((n, P + 1), np.uint8)
+    xs = np.zeros((n, P + 1), np.uint64)
+    os_ = np.zeros((n, P + 1), np.uint64)
+    rc = np.zeros((n, P + 1), np.int32)
+    lib().or_c4_replay(n, P, _i32(a), legal.ctypes.data, status.ctypes.data, xs.ctypes.data, os_.ctypes.data,
+                       _i32(rc))
+    return dict(legal=legal, status=status, x=xs, o=os_, rc=rc)
 
 
 # ---------------------------------------------------------------- net

@@ -147,6 +147,38 @@ void or_c4_bitboards(const or_c4_state *s, uint64_t *x, uint64_t *o) {
     *o = bo;
 }
 
+/* Batch replay for parity tests: game g plays actions[g][0..] until an action
+ * is -1 or illegal.  Per ply p (state BEFORE the p-th action) writes the legal
+ * mask, status and bitboards; returns total plies replayed. */
+long or_c4_replay(int n, int max_plies, const int32_t *actions, uint32_t *legal, uint8_t *status, uint64_t *xs,
+                  uint64_t *os, int32_t *rc) {
+    long total = 0;
+    for (int g = 0; g < n; ++g) {
+        or_c4_state s;
+        or_c4_init(&s);
+        for (int p = 0; p <= max_plies; ++p) {
+            size_t k = (size_t)g * (max_plies + 1) + p;
+            int acts[7];
+            int na = or_c4_valid_actions(&s, acts);
+            uint32_t m = 0;
+            for (int i = 0; i < na; ++i) m |= 1u << acts[i];
+            legal[k] = m;
+            status[k] = s.status;
+            or_c4_bitboards(&s, &xs[k], &os[k]);
+            rc[k] = 0;
+            if (p == max_plies) break;
+            int a = actions[(size_t)g * max_plies + p];
+            if (a < 0) break;
+            or_c4_state nx;
+            rc[k] = or_c4_next_state(&s, a, &nx);
+            if (rc[k] != 0) break;
+            s = nx;
+            ++total;
+        }
+    }
+    return total;
+}
+
 static void c4_init_v(void *s) { or_c4_init((or_c4_state *)s); }
 static int c4_next_v(const void *s, int a, void *o) { return or_c4_next_state((const or_c4_state *)s, a, (or_c4_state *)o); }
 static int c4_valid_v(const void *s, int *a) { return or_c4_valid_actions((const or_c4_state *)s, a); }
@@ -252,6 +284,12 @@ const or_game *or_game_get(int kind) {
     if (kind == OR_GAME_CONNECT4) return &G_C4;
     if (kind == OR_GAME_TICTACTOE) return &G_TTT;
     return NULL;
+}
+
+void or_encode_states(int game, int n, const void *const *states, float *out) {
+    const or_game *g = or_game_get(game);
+    const int E = g->enc_c * g->enc_h * g->enc_w;
+    for (int i = 0; i < n; ++i) g->encoding(states[i], out + (size_t)i * E);
 }
 
 /* ========================================================================

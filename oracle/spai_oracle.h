@@ -72,6 +72,8 @@ typedef struct or_game {
 } or_game;
 
 const or_game *or_game_get(int kind);
+/* get_encoding of n states into out [n][C*H*W] */
+void or_encode_states(int game, int n, const void *const *states, float *out);
 
 /* ndarray 0.15 `sum()` on a contiguous f32 slice (numeric_util::unrolled_fold). */
 float or_nd_sum(const float *x, int n);
@@ -84,6 +86,11 @@ void or_c4_encoding(const or_c4_state *s, float *out);          /* [3][6][7] */
 int or_c4_mask_invalid(const or_c4_state *s, const float *p, int len, float *out);
 /* bitboards in the product's layout: bit (col*7+row) */
 void or_c4_bitboards(const or_c4_state *s, uint64_t *x, uint64_t *o);
+
+/* batch replay of action sequences [n][max_plies] (-1 = stop); per ply p in
+ * [0, max_plies]: legal mask, status, bitboards, next_state rc */
+long or_c4_replay(int n, int max_plies, const int32_t *actions, uint32_t *legal, uint8_t *status, uint64_t *xs,
+                  uint64_t *os, int32_t *rc);
 
 void or_ttt_init(or_ttt_state *s);
 int or_ttt_next_state(const or_ttt_state *s, int action, or_ttt_state *out);

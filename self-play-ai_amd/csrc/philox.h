@@ -1,0 +1,56 @@
+// philox.h — move sampling for self-play (host side).
+//
+// The reference samples a root child with rand::thread_rng and
+// WeightedIndex over visit_count^temperature (learner_concurrent.rs:177,189-193),
+// which is unseeded.  Here the uniform comes from Philox4x32-10 keyed by
+// (seed, game id, move number), so a game's trajectory does not depend on how
+// games are batched or sharded across GPUs; the weights and their running sum
+// are kept in double.  oracle/spai_oracle.c (or_uniform, or_weighted_index)
+// restates the same definition for the parity tests.
+#pragma once
+#include <stdint.h>
+
+#include <cmath>
+
+namespace spai {
+
+inline void philox4x32(uint32_t c[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3], k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1, n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+inline double sample_uniform(uint64_t seed, uint64_t game_id, uint64_t move_no) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t ctr[4] = {(uint32_t)move_no, (uint32_t)(move_no >> 32), (uint32_t)game_id, (uint32_t)(game_id >> 32)};
+    uint32_t out[4];
+    philox4x32(ctr, key, out);
+    uint64_t bits = (((uint64_t)out[0] << 21) ^ ((uint64_t)out[1] >> 11)) & ((1ull << 53) - 1);
+    return (double)bits * (1.0 / 9007199254740992.0);
+}
+
+// index of the sampled child, -1 if n is out of range, -2 if all weights are 0
+inline int weighted_index(const float *visits, int n, float temperature, double u) {
+    double cum[512];
+    double total = 0.0;
+    if (n <= 0 || n > 512) return -1;
+    for (int i = 0; i < n; ++i) {
+        total += std::pow((double)visits[i], (double)temperature);
+        cum[i] = total;
+    }
+    if (!(total > 0.0)) return -2;
+    double x = u * total;
+    for (int i = 0; i < n; ++i)
+        if (cum[i] > x) return i;
+    return n - 1;
+}
+
+}  // namespace spai

@@ -1,0 +1,586 @@
+// search.hip — device-resident MCTS (mcts.rs) + the self-play driver
+// (learner_concurrent.rs:169-242).
+//
+// Trees live in HBM as per-tree arenas of 16-B node records (spai_internal.h).
+// One search iteration (mcts.rs:214-285) is three launches on the engine stream:
+//   k_select        8 lanes per tree (one per child slot): PUCT descent from
+//                   the root, state replayed on bitboards, leaf terminal check;
+//                   terminal leaves are backed up in place, live leaves are
+//                   appended to the batch (wave-aggregated atomic slot).
+//   evaluate        the fused ResNet forward (net_c4.hip) or a stub evaluator.
+//   k_expand        8 lanes per leaf: legal moves by ballot, children packed by
+//                   a per-leaf prefix count, priors written, value backed up
+//                   along the recorded path (lanes split the levels).
+// The host only sees the trees between moves: root visit counts come back once
+// per search call, the sampled child goes down as the new root.
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+
+#include "philox.h"
+#include "spai_internal.h"
+
+namespace spai {
+namespace {
+
+constexpr int kLanesPerTree = 8;
+constexpr int kBlock = 256;
+constexpr int kTreesPerBlock = kBlock / kLanesPerTree;
+constexpr uint32_t kErrNan = 1u, kErrCapacity = 2u, kErrDepth = 4u;
+
+struct TreeView {
+    uint4 *nodes;
+    uint32_t cap;
+    const uint32_t *root;
+    uint32_t *next_free;
+    const uint64_t *root_x, *root_o;
+    const uint8_t *root_n, *root_status;
+    uint32_t *path;
+    uint8_t *depth;
+};
+
+struct BatchView {
+    uint32_t *count;
+    uint32_t *tree;
+    uint64_t *mine, *theirs;
+    float *priors;
+    float *value;
+};
+
+// PUCT score, mcts.rs:91-100, evaluated in the reference's operation order
+// (no contraction: built with -ffp-contract=off; sqrt and / correctly rounded).
+__device__ __forceinline__ float ucb(uint32_t n_parent, const uint4 &ch, float c) {
+    const uint32_t n = ch.x;
+    const float w = __uint_as_float(ch.y), prior = __uint_as_float(ch.z);
+    const float q = n == 0 ? 0.0f : ((-w / (float)n) + 1.0f) / 2.0f;
+    float u = c * prior;
+    u = u * sqrtf((float)n_parent);
+    u = u / (1.0f + (float)n);
+    return q + u;
+}
+
+// backprop (mcts.rs:145-159) over path[0..d]: level d is the leaf (+v), signs
+// alternate upward; lane l of the 8-lane group updates the levels == l (mod 8)
+__device__ __forceinline__ void backup_level(uint4 *nodes, uint32_t node, int d, int lvl, float v) {
+    uint4 *nd = nodes + node;
+    const float sign = ((d - lvl) & 1) ? -1.0f : 1.0f;
+    nd->x = nd->x + 1u;
+    nd->y = __float_as_uint(__uint_as_float(nd->y) + sign * v);
+}
+
+__device__ __forceinline__ void backup(uint4 *nodes, const uint32_t *path, int d, float v, int lane8) {
+    for (int lvl = lane8; lvl <= d; lvl += kLanesPerTree) backup_level(nodes, path[lvl], d, lvl, v);
+}
+
+__global__ __launch_bounds__(kBlock) void k_select(TreeView T, BatchView B, const uint32_t *__restrict__ active,
+                                                   uint32_t n_active, float c, uint32_t *err) {
+    const uint32_t gi = (blockIdx.x * blockDim.x + threadIdx.x) / kLanesPerTree;
+    const int lane8 = threadIdx.x & (kLanesPerTree - 1);
+    if (gi >= n_active) return;
+    const uint32_t t = active[gi];
+    uint4 *nodes = T.nodes + (size_t)t * T.cap;
+    uint32_t *path = T.path + (size_t)t * kMaxDepth;
+    uint32_t node = T.root[t];
+    uint64_t x = T.root_x[t], o = T.root_o[t];
+    uint8_t n = T.root_n[t], status = T.root_status[t];
+    uint4 rec = nodes[node];
+    // path levels == lane8 (mod 8) kept in this lane's registers (kMaxDepth = 6 x 8)
+    uint32_t p0 = node, p1 = 0, p2 = 0, p3 = 0, p4 = 0, p5 = 0;
+    int d = 0;
+    if (lane8 == 0) path[0] = node;
+    bool nan = false;
+    while (rec.w != kNoChildren) {                          // while node.is_fully_expanded()
+        const uint32_t first = rec.w & 0xFFFFFFu, nch = rec.w >> 24;
+        uint4 ch = make_uint4(0, 0, 0, 0);
+        float u = -INFINITY;
+        if ((uint32_t)lane8 < nch) {
+            ch = nodes[first + lane8];
+            u = ucb(rec.x, ch, c);
+            nan |= u != u;
+        }
+        // argmax with ties to the LAST child (Iterator::max_by, mcts.rs:110-113)
+        float bu = u;
+        int bi = lane8;
+#pragma unroll
+        for (int m = 1; m < kLanesPerTree; m <<= 1) {
+            const float ou = __shfl_xor(bu, m, kLanesPerTree);
+            const int oi = __shfl_xor(bi, m, kLanesPerTree);
+            if (ou > bu || (ou == bu && oi > bi)) {
+                bu = ou;
+                bi = oi;
+            }
+        }
+        rec.x = __shfl(ch.x, bi, kLanesPerTree);
+        rec.y = __shfl(ch.y, bi, kLanesPerTree);
+        rec.z = __shfl(ch.z, bi, kLanesPerTree);
+        rec.w = __shfl(ch.w, bi, kLanesPerTree);
+        // replay the child's action on the bitboards (children are in legal-action order)
+        const int a = c4::kth_bit(c4::open_columns(x | o), bi);
+        const uint64_t bit = c4::drop_bit(x | o, a);
+        uint64_t mover;
+        if (c4::x_to_move(n)) { x |= bit; mover = x; }
+        else { o |= bit; mover = o; }
+        n = (uint8_t)(n + 1);
+        status = c4::has_line(mover) ? c4::kWon : (n == c4::kCells ? c4::kTied : c4::kOngoing);
+        node = first + bi;
+        ++d;
+        if (d >= kMaxDepth) {
+            if (lane8 == 0) atomicOr(err, kErrDepth);
+            return;
+        }
+        if ((d & 7) == lane8) {
+            path[d] = node;
+            switch (d >> 3) {
+            case 0: p0 = node; break;
+            case 1: p1 = node; break;
+            case 2: p2 = node; break;
+            case 3: p3 = node; break;
+            case 4: p4 = node; break;
+            default: p5 = node; break;
+            }
+        }
+    }
+    if (nan && lane8 == 0) atomicOr(err, kErrNan);
+    if (lane8 == 0) T.depth[t] = (uint8_t)d;
+    if (status != c4::kOngoing) {                           // terminal leaf: backprop(leaf, value), mcts.rs:245-247
+        const float v = c4::terminal_value(status);
+        const uint32_t pr[6] = {p0, p1, p2, p3, p4, p5};
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            const int lvl = lane8 + 8 * j;
+            if (lvl <= d) backup_level(nodes, pr[j], d, lvl, v);
+        }
+        return;
+    }
+    // live leaf -> batch slot (mcts.rs:249-250)
+    uint32_t slot = 0;
+    if (lane8 == 0) slot = atomicAdd(B.count, 1u);
+    slot = __shfl(slot, 0, kLanesPerTree);
+    if (lane8 == 0) {
+        const bool xm = c4::x_to_move(n);
+        B.tree[slot] = t;
+        B.mine[slot] = xm ? x : o;
+        B.theirs[slot] = xm ? o : x;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_eval_stub(BatchView B, uint32_t max_n, int kind) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= max_n || s >= *B.count) return;
+    // hash evaluator keys on absolute X/O stones: recover them from the player-to-move view
+    const uint32_t n = (uint32_t)c4::popc64(B.mine[s] | B.theirs[s]);
+    const bool xm = (n & 1u) == 0;
+    const uint64_t x = xm ? B.mine[s] : B.theirs[s], o = xm ? B.theirs[s] : B.mine[s];
+    float pr[c4::kActions], v;
+    c4::stub_eval(kind, x, o, (uint8_t)n, pr, &v);
+    for (int a = 0; a < c4::kActions; ++a) B.priors[(size_t)s * kPriorStride + a] = pr[a];
+    B.value[s] = v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_expand(TreeView T, BatchView B, uint32_t max_n, uint32_t *err,
+                                                   uint32_t *iter_count, uint32_t *next_count) {
+    const uint32_t s = (blockIdx.x * blockDim.x + threadIdx.x) / kLanesPerTree;
+    const int lane8 = threadIdx.x & (kLanesPerTree - 1);
+    const uint32_t count = *B.count;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        *iter_count = count;   // per-iteration evaluated leaves
+        *next_count = 0u;      // the next iteration's batch counter (double-buffered)
+    }
+    if (s >= max_n || s >= count) return;
+    const uint32_t t = B.tree[s];
+    uint4 *nodes = T.nodes + (size_t)t * T.cap;
+    const uint32_t *path = T.path + (size_t)t * kMaxDepth;
+    const int d = T.depth[t];
+    const uint32_t leaf = path[d];
+    const uint64_t occ = B.mine[s] | B.theirs[s];
+    // legal actions of the (live) leaf; children in ascending action order (mcts.rs:116-143)
+    const bool legal = lane8 < c4::kActions && !((occ >> (7 * lane8 + 5)) & 1ull);
+    const uint64_t ball = __ballot(legal);
+    const uint32_t grp = (uint32_t)(ball >> (threadIdx.x & 63 & ~(kLanesPerTree - 1))) & 0xFFu;
+    const uint32_t nch = c4::popc32(grp);
+    const uint32_t idx = c4::popc32(grp & ((1u << lane8) - 1u));
+    const uint32_t first = T.next_free[t];
+    if (first + nch > T.cap) {
+        if (lane8 == 0) atomicOr(err, kErrCapacity);
+        return;
+    }
+    if (legal) nodes[first + idx] = make_uint4(0u, 0u, __float_as_uint(B.priors[(size_t)s * kPriorStride + lane8]),
+                                               kNoChildren);
+    if (lane8 == 0) {
+        T.next_free[t] = first + nch;
+        nodes[leaf].w = first | (nch << 24);
+    }
+    backup(nodes, path, d, B.value[s], lane8);
+}
+
+// per active tree: [0] = root first|nch<<24 (children word), [1..7] child visit counts
+__global__ void k_root_stats(TreeView T, const uint32_t *__restrict__ active, uint32_t n_active, uint32_t *out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_active) return;
+    const uint32_t t = active[i];
+    const uint4 *nodes = T.nodes + (size_t)t * T.cap;
+    const uint4 r = nodes[T.root[t]];
+    out[i * 8] = r.w;
+    const uint32_t nch = r.w == kNoChildren ? 0 : r.w >> 24, first = r.w & 0xFFFFFFu;
+    for (uint32_t k = 0; k < 7; ++k) out[i * 8 + 1 + k] = k < nch ? nodes[first + k].x : 0u;
+}
+
+__global__ void k_trees_init(TreeView T, uint32_t first_tree, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t t = first_tree + i;
+    T.nodes[(size_t)t * T.cap] = make_uint4(0u, 0u, 0u, kNoChildren);
+    T.next_free[t] = 1;
+}
+
+TreeView tree_view(spai_engine *e) {
+    Trees &T = e->trees;
+    return TreeView{T.nodes.p, T.cap, T.root.p, T.next_free.p, T.root_x.p, T.root_o.p, T.root_n.p, T.root_status.p,
+                    T.path.p, T.depth.p};
+}
+
+BatchView batch_view(spai_engine *e, uint32_t slot) {
+    Batch &B = e->batch;
+    return BatchView{B.count.p + slot, B.tree.p, B.mine.p, B.theirs.p, B.priors.p, B.value.p};
+}
+
+// upload host root bookkeeping for trees [t0, t0+n)
+int upload_roots(spai_engine *e, uint32_t t0, uint32_t n) {
+    Trees &T = e->trees;
+    std::vector<uint64_t> x(n), o(n);
+    std::vector<uint8_t> nn(n), st(n);
+    for (uint32_t i = 0; i < n; ++i) {
+        const c4::State &s = T.h_root_state[t0 + i];
+        x[i] = s.x;
+        o[i] = s.o;
+        nn[i] = s.n;
+        st[i] = s.status;
+    }
+    hipStream_t s = e->stream;
+    SPAI_HIP(hipMemcpyAsync(T.root.p + t0, T.h_root.data() + t0, n * 4, hipMemcpyHostToDevice, s));
+    SPAI_HIP(hipMemcpyAsync(T.root_x.p + t0, x.data(), n * 8, hipMemcpyHostToDevice, s));
+    SPAI_HIP(hipMemcpyAsync(T.root_o.p + t0, o.data(), n * 8, hipMemcpyHostToDevice, s));
+    SPAI_HIP(hipMemcpyAsync(T.root_n.p + t0, nn.data(), n, hipMemcpyHostToDevice, s));
+    SPAI_HIP(hipMemcpyAsync(T.root_status.p + t0, st.data(), n, hipMemcpyHostToDevice, s));
+    SPAI_HIP(hipStreamSynchronize(s));
+    return SPAI_OK;
+}
+
+int timer_record(spai_engine *e, int which, uint32_t iter, bool begin) {
+    KernelTimer &K = e->timer;
+    if (!K.enabled) return SPAI_OK;
+    if (begin) {
+        if (K.used + 2 > K.ev.size()) {
+            for (int i = 0; i < 64; ++i) {
+                hipEvent_t ev;
+                SPAI_HIP(hipEventCreate(&ev));
+                K.ev.push_back(ev);
+            }
+        }
+        K.which.push_back(which);
+        K.iter.push_back(iter);
+        SPAI_HIP(hipEventRecord(K.ev[K.used], e->stream));
+    } else {
+        SPAI_HIP(hipEventRecord(K.ev[K.used + 1], e->stream));
+        K.used += 2;
+    }
+    return SPAI_OK;
+}
+
+// fold the sampled event pairs of one search call into the totals
+int timer_collect(spai_engine *e, const std::vector<uint32_t> &iter_counts, uint32_t n_active) {
+    KernelTimer &K = e->timer;
+    if (!K.enabled) return SPAI_OK;
+    for (size_t i = 0; i < K.which.size(); ++i) {
+        float ms = 0;
+        SPAI_HIP(hipEventElapsedTime(&ms, K.ev[2 * i], K.ev[2 * i + 1]));
+        const int w = K.which[i];
+        K.total_ms[w] += ms;
+        K.launches[w] += 1;
+        K.items[w] += w == 0 ? n_active : iter_counts[K.iter[i]];
+    }
+    K.used = 0;
+    K.which.clear();
+    K.iter.clear();
+    return SPAI_OK;
+}
+
+}  // namespace
+
+int trees_create(spai_engine *e, uint32_t n) {
+    SPAI_CHECK(n > 0 && n <= e->cfg.max_trees, SPAI_ERR_INVALID, "trees_create: n=%u exceeds max_trees=%u", n,
+               e->cfg.max_trees);
+    Trees &T = e->trees;
+    // worst case: one expansion of <= 7 children per search iteration for every ply of the game
+    const uint64_t cap = 1ull + (uint64_t)c4::kActions * e->cfg.num_searches * std::max(1u, e->cfg.max_moves);
+    SPAI_CHECK(cap < (1ull << 24), SPAI_ERR_CAPACITY, "node arena of %llu nodes per tree exceeds 2^24",
+               (unsigned long long)cap);
+    if (T.n_trees != n || T.cap != cap) {
+        T.n_trees = 0;
+        SPAI_TRY(T.nodes.alloc((size_t)n * cap));
+        SPAI_TRY(T.root.alloc(n));
+        SPAI_TRY(T.next_free.alloc(n));
+        SPAI_TRY(T.root_x.alloc(n));
+        SPAI_TRY(T.root_o.alloc(n));
+        SPAI_TRY(T.root_n.alloc(n));
+        SPAI_TRY(T.root_status.alloc(n));
+        SPAI_TRY(T.path.alloc((size_t)n * kMaxDepth));
+        SPAI_TRY(T.depth.alloc(n));
+        SPAI_TRY(e->active.alloc(n));
+        SPAI_TRY(e->stats.alloc((size_t)n * 8));
+        Batch &B = e->batch;
+        SPAI_TRY(B.count.alloc(2));
+        SPAI_TRY(B.tree.alloc(n));
+        SPAI_TRY(B.mine.alloc(n));
+        SPAI_TRY(B.theirs.alloc(n));
+        SPAI_TRY(B.priors.alloc((size_t)n * kPriorStride));
+        SPAI_TRY(B.value.alloc(n));
+        B.cap = n;
+        T.n_trees = n;
+        T.cap = (uint32_t)cap;
+    }
+    T.h_root.assign(n, 0);
+    T.h_root_state.assign(n, c4::State{0, 0, 0, c4::kOngoing});
+    T.h_root_first.assign(n, 0);
+    T.h_root_nch.assign(n, 0);
+    k_trees_init<<<(n + 255) / 256, 256, 0, e->stream>>>(tree_view(e), 0, n);
+    SPAI_HIP(hipGetLastError());
+    return upload_roots(e, 0, n);
+}
+
+int tree_reset(spai_engine *e, uint32_t t, const spai_c4_state *root) {
+    Trees &T = e->trees;
+    SPAI_CHECK(t < T.n_trees, SPAI_ERR_INVALID, "tree %u out of range", t);
+    c4::State s{0, 0, 0, c4::kOngoing};
+    if (root) {
+        SPAI_CHECK(!(root->x & root->o) && !((root->x | root->o) & ~c4::kBoard) && root->status <= c4::kWon,
+                   SPAI_ERR_INVALID, "root is not a Connect4 bitboard");
+        s = from_abi(*root);
+    }
+    T.h_root[t] = 0;
+    T.h_root_state[t] = s;
+    T.h_root_first[t] = 0;
+    T.h_root_nch[t] = 0;
+    k_trees_init<<<1, 64, 0, e->stream>>>(tree_view(e), t, 1);
+    SPAI_HIP(hipGetLastError());
+    return upload_roots(e, t, 1);
+}
+
+int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_searches, float *policy,
+           uint32_t *child_ids, float *child_visits, uint32_t *n_children, double *evals_out) {
+    Trees &T = e->trees;
+    SPAI_CHECK(T.n_trees > 0, SPAI_ERR_INVALID, "no trees: call spai_trees_create first");
+    SPAI_CHECK(n <= T.n_trees, SPAI_ERR_INVALID, "search over %u trees, %u exist", n, T.n_trees);
+    for (uint32_t i = 0; i < n; ++i) SPAI_CHECK(tree_idx[i] < T.n_trees, SPAI_ERR_INVALID, "tree %u out of range", tree_idx[i]);
+    const int kind = (int)e->cfg.eval;
+    SPAI_CHECK(kind != SPAI_EVAL_NET || e->net, SPAI_ERR_INVALID, "eval = NET but no net set (spai_engine_set_net)");
+    if (n == 0) return SPAI_OK;
+    hipStream_t st = e->stream;
+    Batch &B = e->batch;
+    if (B.iter_counts.n < num_searches) SPAI_TRY(B.iter_counts.alloc(std::max<uint32_t>(num_searches, 1)));
+    SPAI_HIP(hipMemcpyAsync(e->active.p, tree_idx, n * 4, hipMemcpyHostToDevice, st));
+    SPAI_HIP(hipMemsetAsync(e->err.p, 0, 4, st));
+    SPAI_HIP(hipMemsetAsync(B.count.p, 0, 8, st));
+    const TreeView tv = tree_view(e);
+    const uint32_t g8 = (n + kTreesPerBlock - 1) / kTreesPerBlock;
+    const bool timed = e->timer.enabled;
+    for (uint32_t it = 0; it < num_searches; ++it) {
+        const bool sample = timed && (it % 4 == 0);
+        const uint32_t cur = it & 1u;
+        const BatchView bv = batch_view(e, cur);
+        if (sample) SPAI_TRY(timer_record(e, 0, it, true));
+        k_select<<<g8, kBlock, 0, st>>>(tv, bv, e->active.p, n, e->cfg.c, e->err.p);
+        if (sample) SPAI_TRY(timer_record(e, 0, it, false));
+        if (sample) SPAI_TRY(timer_record(e, 1, it, true));
+        if (kind == SPAI_EVAL_NET) {
+            SPAI_TRY(net_eval_batch(e->net, st, bv.count, n, B.mine.p, B.theirs.p, B.priors.p, B.value.p));
+        } else {
+            k_eval_stub<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(bv, n, kind);
+        }
+        if (sample) SPAI_TRY(timer_record(e, 1, it, false));
+        if (sample) SPAI_TRY(timer_record(e, 2, it, true));
+        k_expand<<<g8, kBlock, 0, st>>>(tv, bv, n, e->err.p, B.iter_counts.p + it, B.count.p + (cur ^ 1u));
+        if (sample) SPAI_TRY(timer_record(e, 2, it, false));
+    }
+    SPAI_HIP(hipGetLastError());
+    k_root_stats<<<(n + 255) / 256, 256, 0, st>>>(tv, e->active.p, n, e->stats.p);
+    SPAI_HIP(hipGetLastError());
+    std::vector<uint32_t> stats((size_t)n * 8), counts(num_searches);
+    uint32_t err = 0;
+    SPAI_HIP(hipMemcpyAsync(stats.data(), e->stats.p, stats.size() * 4, hipMemcpyDeviceToHost, st));
+    if (num_searches)
+        SPAI_HIP(hipMemcpyAsync(counts.data(), B.iter_counts.p, num_searches * 4, hipMemcpyDeviceToHost, st));
+    SPAI_HIP(hipMemcpyAsync(&err, e->err.p, 4, hipMemcpyDeviceToHost, st));
+    SPAI_HIP(hipStreamSynchronize(st));
+    SPAI_TRY(timer_collect(e, counts, n));
+    SPAI_CHECK(!(err & kErrCapacity), SPAI_ERR_CAPACITY, "node arena full (cap %u per tree)", T.cap);
+    SPAI_CHECK(!(err & kErrDepth), SPAI_ERR_CAPACITY, "tree deeper than %d", kMaxDepth);
+    SPAI_CHECK(!(err & kErrNan), SPAI_ERR_NAN, "NaN UCB in select (reference: partial_cmp().unwrap() panics)");
+    if (evals_out) {
+        double s = 0;
+        for (uint32_t c : counts) s += c;
+        *evals_out = s;
+    }
+    // root visit policy (mcts.rs:310-331)
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t t = tree_idx[i];
+        const uint32_t w = stats[i * 8];
+        const uint32_t nch = w == kNoChildren ? 0 : w >> 24, first = w & 0xFFFFFFu;
+        T.h_root_first[t] = first;
+        T.h_root_nch[t] = (uint8_t)nch;
+        const c4::State &rs = T.h_root_state[t];
+        const uint32_t legal = c4::legal_mask(rs.x, rs.o, rs.status);
+        float pol[c4::kActions] = {0, 0, 0, 0, 0, 0, 0};
+        for (uint32_t k = 0; k < nch; ++k) {
+            const float v = (float)stats[i * 8 + 1 + k];
+            pol[c4::kth_bit(legal, (int)k)] = v;
+            if (child_ids) child_ids[(size_t)i * 7 + k] = first + k;
+            if (child_visits) child_visits[(size_t)i * 7 + k] = v;
+        }
+        for (uint32_t k = nch; k < 7; ++k) {
+            if (child_ids) child_ids[(size_t)i * 7 + k] = kNoChildren;
+            if (child_visits) child_visits[(size_t)i * 7 + k] = 0.f;
+        }
+        if (n_children) n_children[i] = nch;
+        if (policy) {
+            float s = 0.0f;   // Policy::normalize: ndarray sum (sequential for 7) then divide
+            for (int a = 0; a < c4::kActions; ++a) s = s + pol[a];
+            for (int a = 0; a < c4::kActions; ++a) policy[(size_t)i * 7 + a] = pol[a] / s;
+        }
+    }
+    return SPAI_OK;
+}
+
+int tree_use_subtree(spai_engine *e, uint32_t t, uint32_t child) {
+    Trees &T = e->trees;
+    SPAI_CHECK(t < T.n_trees, SPAI_ERR_INVALID, "tree %u out of range", t);
+    const uint32_t first = T.h_root_first[t], nch = T.h_root_nch[t];
+    SPAI_CHECK(nch > 0 && child >= first && child < first + nch, SPAI_ERR_INVALID,
+               "node %u is not a child of tree %u's root (run spai_search first)", child, t);
+    const c4::State &rs = T.h_root_state[t];
+    c4::State ns;
+    const int a = c4::kth_bit(c4::legal_mask(rs.x, rs.o, rs.status), (int)(child - first));
+    SPAI_CHECK(c4::next_state(rs, a, ns) == 0, SPAI_ERR_INVALID, "internal: root child replay failed");
+    T.h_root[t] = child;
+    T.h_root_state[t] = ns;
+    T.h_root_nch[t] = 0;
+    return upload_roots(e, t, 1);
+}
+
+int tree_node(spai_engine *e, uint32_t t, uint32_t node, spai_c4_state *st, uint32_t *visits, float *w) {
+    Trees &T = e->trees;
+    SPAI_CHECK(t < T.n_trees, SPAI_ERR_INVALID, "tree %u out of range", t);
+    c4::State s = T.h_root_state[t];
+    if (node != T.h_root[t]) {
+        const uint32_t first = T.h_root_first[t], nch = T.h_root_nch[t];
+        SPAI_CHECK(nch > 0 && node >= first && node < first + nch, SPAI_ERR_INVALID,
+                   "node %u: only the root and its children are addressable", node);
+        const int a = c4::kth_bit(c4::legal_mask(s.x, s.o, s.status), (int)(node - first));
+        c4::State ns;
+        c4::next_state(s, a, ns);
+        s = ns;
+    }
+    if (st) *st = to_abi(s);
+    if (visits || w) {
+        uint4 rec;
+        SPAI_HIP(hipMemcpy(&rec, T.nodes.p + (size_t)t * T.cap + node, 16, hipMemcpyDeviceToHost));
+        if (visits) *visits = rec.x;
+        if (w) memcpy(w, &rec.y, 4);
+    }
+    return SPAI_OK;
+}
+
+int tree_size(spai_engine *e, uint32_t t, uint32_t *nodes) {
+    Trees &T = e->trees;
+    SPAI_CHECK(t < T.n_trees, SPAI_ERR_INVALID, "tree %u out of range", t);
+    SPAI_HIP(hipMemcpy(nodes, T.next_free.p + t, 4, hipMemcpyDeviceToHost));
+    return SPAI_OK;
+}
+
+// SelfPlayWorker::self_play (learner_concurrent.rs:169-242)
+int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sample_sink sink, void *user,
+                 spai_selfplay_stats *stats) {
+    const auto t_start = std::chrono::steady_clock::now();
+    SPAI_TRY(trees_create(e, n_games));
+    Trees &T = e->trees;
+    struct Hist {
+        std::vector<c4::State> states;
+        std::vector<float> policies;
+        std::vector<int32_t> moves;
+    };
+    std::vector<Hist> hist(n_games);
+    std::vector<uint32_t> active(n_games);
+    for (uint32_t i = 0; i < n_games; ++i) active[i] = i;
+    std::vector<float> pol((size_t)n_games * 7), vis((size_t)n_games * 7);
+    std::vector<uint32_t> ids((size_t)n_games * 7), nch(n_games);
+    std::vector<float> enc, sp, sv;
+    double sims = 0, evals = 0, games = 0, positions = 0, moves = 0;
+    uint64_t move_no = 0;
+    while (!active.empty()) {
+        const uint32_t na = (uint32_t)active.size();
+        double ev = 0;
+        SPAI_TRY(search(e, na, active.data(), e->cfg.num_searches, pol.data(), ids.data(), vis.data(), nch.data(), &ev));
+        sims += (double)na * e->cfg.num_searches;
+        evals += ev;
+        moves += 1;
+        for (int k = (int)na - 1; k >= 0; --k) {              // for i in (0..trees_vec.len()).rev()
+            const uint32_t t = active[k];
+            Hist &h = hist[t];
+            const double u = sample_uniform(e->cfg.seed, gid_base + t, move_no);
+            const int idx = weighted_index(vis.data() + (size_t)k * 7, (int)nch[k], e->cfg.temperature, u);
+            SPAI_CHECK(idx >= 0, SPAI_ERR_NAN, "WeightedIndex over all-zero visit counts (game %u)", t);
+            const c4::State rs = T.h_root_state[t];
+            const int a = c4::kth_bit(c4::legal_mask(rs.x, rs.o, rs.status), idx);
+            c4::State cs;
+            c4::next_state(rs, a, cs);
+            h.states.push_back(rs);
+            h.policies.insert(h.policies.end(), pol.begin() + (size_t)k * 7, pol.begin() + (size_t)k * 7 + 7);
+            h.moves.push_back(a);
+            if (cs.status != c4::kOngoing) {                  // is_terminal: emit, trees_vec.remove(i)
+                const float v = c4::terminal_value(cs.status);
+                const size_t m = h.states.size();
+                enc.assign(m * 126, 0.f);
+                sv.resize(m);
+                for (size_t j = 0; j < m; ++j) {
+                    const c4::State &s = h.states[j];
+                    const bool xm = c4::x_to_move(s.n);
+                    const uint64_t mine = xm ? s.x : s.o, theirs = xm ? s.o : s.x;
+                    for (int r = 0; r < 6; ++r)
+                        for (int cc = 0; cc < 7; ++cc) {
+                            const int b = cc * 7 + r, cell = r * 7 + cc;
+                            if ((mine >> b) & 1) enc[j * 126 + cell] = 1.f;
+                            else if ((theirs >> b) & 1) enc[j * 126 + 42 + cell] = 1.f;
+                            else enc[j * 126 + 84 + cell] = 1.f;
+                        }
+                    // x.get_current_player() == state.get_current_player() ? value : -value
+                    sv[j] = ((s.n & 1) == (cs.n & 1)) ? v : -v;
+                }
+                if (sink) sink(user, (uint32_t)(gid_base + t), (uint32_t)m, enc.data(), h.policies.data(), sv.data(),
+                               h.moves.data());
+                games += 1;
+                positions += (double)m;
+                Hist().states.swap(h.states);
+                h.policies.clear();
+                h.moves.clear();
+                active.erase(active.begin() + k);
+            } else {                                          // use_subtree(selected_id)
+                T.h_root[t] = T.h_root_first[t] + (uint32_t)idx;
+                T.h_root_state[t] = cs;
+                T.h_root_nch[t] = 0;
+            }
+        }
+        SPAI_TRY(upload_roots(e, 0, T.n_trees));
+        ++move_no;
+    }
+    if (stats) {
+        stats->sims = sims;
+        stats->evals = evals;
+        stats->games = games;
+        stats->positions = positions;
+        stats->moves = moves;
+        stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+    }
+    return SPAI_OK;
+}
+
+}  // namespace spai

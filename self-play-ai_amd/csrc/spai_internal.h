@@ -1,0 +1,185 @@
+// spai_internal.h — engine state shared by the HIP translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/spai.h"
+#include "c4.h"
+
+namespace spai {
+
+void set_error(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+
+#define SPAI_HIP(expr)                                                                                  \
+    do {                                                                                                \
+        hipError_t e_ = (expr);                                                                         \
+        if (e_ != hipSuccess) {                                                                         \
+            ::spai::set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+            return SPAI_ERR_DEVICE;                                                                     \
+        }                                                                                               \
+    } while (0)
+
+#define SPAI_CHECK(cond, code, ...)          \
+    do {                                     \
+        if (!(cond)) {                       \
+            ::spai::set_error(__VA_ARGS__);  \
+            return (code);                   \
+        }                                    \
+    } while (0)
+
+#define SPAI_TRY(expr)             \
+    do {                           \
+        int rc_ = (expr);          \
+        if (rc_ != SPAI_OK) return rc_; \
+    } while (0)
+
+template <class T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    int alloc(size_t count) {
+        release();
+        if (count == 0) return SPAI_OK;
+        SPAI_HIP(hipMalloc((void **)&p, count * sizeof(T)));
+        n = count;
+        return SPAI_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+// Node record, 16 B, one per tree node (mcts.rs:20-30 without the State clone):
+//   x = visit_count (u32), y = value_sum (f32 bits), z = prior (f32 bits),
+//   w = children: kNoChildren, or first_child (24 bits, per-tree index) | n_children << 24.
+// Children of a node are contiguous and in legal-action order, so a child's
+// action and state follow from its parent's state (no per-node State copy).
+constexpr uint32_t kNoChildren = 0xFFFFFFFFu;
+constexpr int kMaxDepth = 48;        // >= 42 plies + root
+constexpr int kPriorStride = 8;      // priors [slot][8]
+
+// Game slots for the batched rules API (SoA bitboards in HBM).
+struct GameSlots {
+    DevBuf<uint64_t> x, o;
+    DevBuf<uint8_t> n, status;
+    uint32_t count = 0;
+};
+
+// Device-resident MCTS trees, one arena of `cap` nodes per tree.
+struct Trees {
+    uint32_t n_trees = 0;
+    uint32_t cap = 0;
+    DevBuf<uint4> nodes;            // [n_trees * cap]
+    DevBuf<uint32_t> root;          // root node index per tree
+    DevBuf<uint32_t> next_free;     // arena fill per tree
+    DevBuf<uint64_t> root_x, root_o;
+    DevBuf<uint8_t> root_n, root_status;
+    DevBuf<uint32_t> path;          // [n_trees * kMaxDepth]
+    DevBuf<uint8_t> depth;          // [n_trees]
+    // host mirrors of the root bookkeeping
+    std::vector<uint32_t> h_root;
+    std::vector<c4::State> h_root_state;
+    std::vector<uint32_t> h_root_first;   // first child of the root after the last search
+    std::vector<uint8_t> h_root_nch;
+};
+
+// One search iteration's leaf batch (the evaluator's input/output).
+struct Batch {
+    uint32_t cap = 0;
+    DevBuf<uint32_t> count;         // [1]
+    DevBuf<uint32_t> tree;          // slot -> tree
+    DevBuf<uint64_t> mine, theirs;  // leaf position, player-to-move view
+    DevBuf<float> priors;           // [cap][8] masked softmax
+    DevBuf<float> value;            // [cap]
+    DevBuf<uint32_t> iter_counts;   // per-iteration leaf counts of the current search
+};
+
+struct KernelTimer {
+    bool enabled = false;
+    double total_ms[3] = {0, 0, 0};
+    double launches[3] = {0, 0, 0};
+    double items[3] = {0, 0, 0};
+    std::vector<hipEvent_t> ev;     // pool, 2 per sampled launch
+    size_t used = 0;
+    std::vector<int> which;         // kernel index per sampled launch
+    std::vector<uint32_t> iter;     // iteration per sampled launch
+};
+
+}  // namespace spai
+
+struct spai_net {
+    spai_engine *eng = nullptr;
+    int blocks = 0, hidden = 0;
+    // packed, BN-folded bf16 MFMA fragments + fp32 biases / head linears (see net_c4.hip)
+    spai::DevBuf<uint16_t> w_stem, w_res, w_head;
+    spai::DevBuf<float> b_stem, b_res, b_head, w_pol, b_pol, w_val, b_val;
+    spai::DevBuf<float> io_x, io_logits, io_value, io_priors;   // scratch for forward/predict calls
+    spai::DevBuf<uint64_t> io_mine, io_theirs;
+    spai::DevBuf<uint32_t> io_count;
+};
+
+struct spai_engine {
+    int game = SPAI_GAME_CONNECT4;
+    int device = 0;
+    spai_config cfg{};
+    hipStream_t stream = nullptr;
+    spai::GameSlots games;
+    spai::Trees trees;
+    spai::Batch batch;
+    spai_net *net = nullptr;
+    spai::DevBuf<uint32_t> active;   // active tree list
+    spai::DevBuf<uint32_t> err;      // device error flags
+    spai::DevBuf<uint32_t> stats;    // root stats [n][8]
+    spai::KernelTimer timer;
+};
+
+namespace spai {
+// rules.hip
+int rules_resize(spai_engine *e, uint32_t n);
+int rules_reset(spai_engine *e, uint32_t first, uint32_t n);
+int rules_write(spai_engine *e, uint32_t first, uint32_t n, const spai_c4_state *s);
+int rules_read(spai_engine *e, uint32_t first, uint32_t n, spai_c4_state *s);
+int rules_legal(spai_engine *e, uint32_t first, uint32_t n, uint32_t *mask);
+int rules_apply(spai_engine *e, uint32_t first, uint32_t n, const int32_t *actions, int32_t *rc);
+int rules_value_term(spai_engine *e, uint32_t first, uint32_t n, float *v, uint8_t *t);
+int rules_encode(spai_engine *e, uint32_t first, uint32_t n, float *out);
+int rules_mask(spai_engine *e, uint32_t first, uint32_t n, const float *p, uint32_t len, float *out);
+int rules_bench(spai_engine *e, uint32_t n, uint32_t iters, double *ms);
+
+// net_c4.hip
+int net_create(spai_engine *e, int blocks, int hidden, const float *params, size_t nparams, spai_net **out);
+void net_destroy(spai_net *net);
+int net_forward_x(spai_net *net, uint32_t n, const float *x, float *logits, float *value);
+int net_predict(spai_net *net, uint32_t n, const spai_c4_state *states, float *priors, float *values);
+size_t net_num_params(int game, int blocks, int hidden);
+void net_init_params(int game, int blocks, int hidden, uint64_t seed, float *params);
+// evaluate `count` (device scalar) leaves of the batch; grid sized for max_n
+int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint32_t max_n,
+                   const uint64_t *mine, const uint64_t *theirs, float *priors, float *value);
+
+// search.hip
+int trees_create(spai_engine *e, uint32_t n);
+int tree_reset(spai_engine *e, uint32_t t, const spai_c4_state *root);
+int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_searches, float *policy,
+           uint32_t *child_ids, float *child_visits, uint32_t *n_children, double *evals_out);
+int tree_use_subtree(spai_engine *e, uint32_t t, uint32_t child);
+int tree_node(spai_engine *e, uint32_t t, uint32_t node, spai_c4_state *st, uint32_t *visits, float *w);
+int tree_size(spai_engine *e, uint32_t t, uint32_t *nodes);
+int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sample_sink sink, void *user,
+                 spai_selfplay_stats *stats);
+
+inline c4::State from_abi(const spai_c4_state &s) { return c4::State{s.x, s.o, s.num_actions_played, s.status}; }
+inline spai_c4_state to_abi(const c4::State &s) {
+    spai_c4_state r{};
+    r.x = s.x;
+    r.o = s.o;
+    r.num_actions_played = s.n;
+    r.status = s.status;
+    return r;
+}
+}  // namespace spai

@@ -1,0 +1,335 @@
+"""ctypes binding of libspai.so (include/spai.h) — the Python face of the engine.
+
+Mirrors the reference's hot-path surface (joshua16266261/self-play-ai):
+  State (game/connect_four.rs)     -> Engine.games_* / legal_mask / apply / encode / mask_invalid
+  Net + Model::predict (model/)    -> Net.forward / Net.predict
+  Tree + Mcts::search (mcts.rs)    -> Engine.trees_create / search / use_subtree
+  SelfPlayWorker::self_play        -> Engine.self_play
+Every call goes through the HIP library; there is no CPU fallback.  Importing
+this module on a machine without the built library raises immediately.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libspai.so")
+
+GAME_TICTACTOE, GAME_CONNECT4, GAME_CHESS = 0, 1, 2
+EVAL_NET, EVAL_UNIFORM, EVAL_HASH = 0, 1, 2
+ONGOING, TIED, WON = 0, 1, 2
+OK = 0
+ERRORS = {-1: "INVALID", -2: "ILLEGAL_MOVE", -3: "GAME_OVER", -4: "DEVICE", -5: "NAN", -6: "CAPACITY",
+          -7: "UNSUPPORTED"}
+
+# every symbol declared in include/spai.h
+SYMBOLS = [
+    "spai_last_error", "spai_version", "spai_device_count", "spai_config_default", "spai_engine_create",
+    "spai_engine_destroy", "spai_engine_sync", "spai_games_resize", "spai_games_reset", "spai_games_write",
+    "spai_games_read", "spai_legal_mask", "spai_apply", "spai_value_terminated", "spai_encode",
+    "spai_mask_invalid", "spai_rules_bench", "spai_net_num_params", "spai_net_init_params", "spai_net_create",
+    "spai_net_destroy", "spai_net_forward", "spai_predict", "spai_engine_set_net", "spai_trees_create",
+    "spai_tree_reset", "spai_search", "spai_tree_use_subtree", "spai_tree_node", "spai_tree_size",
+    "spai_selfplay_run", "spai_engine_set_timing", "spai_engine_timing", "spai_engine_timing_items",
+]
+
+
+class SpaiError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"spai error {code} ({ERRORS.get(code, '?')}): {msg}")
+        self.code = code
+
+
+class C4State(C.Structure):
+    _fields_ = [("x", C.c_uint64), ("o", C.c_uint64), ("num_actions_played", C.c_uint8), ("status", C.c_uint8),
+                ("pad", C.c_uint8 * 6)]
+
+
+class Config(C.Structure):
+    _fields_ = [("c", C.c_float), ("num_searches", C.c_uint32), ("temperature", C.c_float),
+                ("max_trees", C.c_uint32), ("max_moves", C.c_uint32), ("eval", C.c_uint32), ("seed", C.c_uint64)]
+
+
+class SelfPlayStats(C.Structure):
+    _fields_ = [(k, C.c_double) for k in ("sims", "evals", "games", "positions", "moves", "seconds")]
+
+
+SINK = C.CFUNCTYPE(None, C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                   C.POINTER(C.c_float), C.POINTER(C.c_int32))
+
+C4_STATE_DTYPE = np.dtype([("x", "<u8"), ("o", "<u8"), ("n", "u1"), ("status", "u1"), ("pad", "u1", 6)])
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `make -C self-play-ai_amd` (hipcc, gfx950)")
+        L = C.CDLL(LIB_PATH)
+        vp, u32, u64, i32 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int
+        P = C.POINTER
+        for name in SYMBOLS:
+            getattr(L, name).restype = C.c_int
+        L.spai_last_error.restype = C.c_char_p
+        L.spai_version.restype = C.c_char_p
+        L.spai_device_count.argtypes = [P(C.c_int)]
+        L.spai_config_default.argtypes = [i32, P(Config)]
+        L.spai_engine_create.argtypes = [i32, P(Config), i32, P(vp)]
+        L.spai_engine_destroy.argtypes = [vp]
+        L.spai_engine_sync.argtypes = [vp]
+        L.spai_games_resize.argtypes = [vp, u32]
+        L.spai_games_reset.argtypes = [vp, u32, u32]
+        L.spai_games_write.argtypes = [vp, u32, u32, vp]
+        L.spai_games_read.argtypes = [vp, u32, u32, vp]
+        L.spai_legal_mask.argtypes = [vp, u32, u32, vp]
+        L.spai_apply.argtypes = [vp, u32, u32, vp, vp]
+        L.spai_value_terminated.argtypes = [vp, u32, u32, vp, vp]
+        L.spai_encode.argtypes = [vp, u32, u32, vp]
+        L.spai_mask_invalid.argtypes = [vp, u32, u32, vp, u32, vp]
+        L.spai_rules_bench.argtypes = [vp, u32, u32, vp]
+        L.spai_net_num_params.argtypes = [i32, i32, i32, P(C.c_size_t)]
+        L.spai_net_init_params.argtypes = [i32, i32, i32, u64, vp]
+        L.spai_net_create.argtypes = [vp, i32, i32, vp, C.c_size_t, P(vp)]
+        L.spai_net_destroy.argtypes = [vp]
+        L.spai_net_forward.argtypes = [vp, u32, vp, vp, vp]
+        L.spai_predict.argtypes = [vp, u32, vp, vp, vp]
+        L.spai_engine_set_net.argtypes = [vp, vp]
+        L.spai_trees_create.argtypes = [vp, u32]
+        L.spai_tree_reset.argtypes = [vp, u32, vp]
+        L.spai_search.argtypes = [vp, u32, vp, u32, vp, vp, vp, vp]
+        L.spai_tree_use_subtree.argtypes = [vp, u32, u32]
+        L.spai_tree_node.argtypes = [vp, u32, u32, vp, vp, vp]
+        L.spai_tree_size.argtypes = [vp, u32, vp]
+        L.spai_selfplay_run.argtypes = [vp, u32, u64, SINK, vp, P(SelfPlayStats)]
+        L.spai_engine_set_timing.argtypes = [vp, i32]
+        L.spai_engine_timing.argtypes = [vp, vp, vp]
+        L.spai_engine_timing_items.argtypes = [vp, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != OK:
+        raise SpaiError(rc, lib().spai_last_error().decode())
+    return rc
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def device_count():
+    n = C.c_int()
+    _check(lib().spai_device_count(C.byref(n)))
+    return n.value
+
+
+def num_params(blocks, hidden=64, game=GAME_CONNECT4):
+    n = C.c_size_t()
+    _check(lib().spai_net_num_params(game, blocks, hidden, C.byref(n)))
+    return n.value
+
+
+def init_params(blocks, hidden=64, seed=0, game=GAME_CONNECT4):
+    p = np.zeros(num_params(blocks, hidden, game), np.float32)
+    _check(lib().spai_net_init_params(game, blocks, hidden, seed, _p(p)))
+    return p
+
+
+def states_array(states):
+    """list of (x, o, n, status) or an existing structured array -> C4_STATE_DTYPE array"""
+    if isinstance(states, np.ndarray) and states.dtype == C4_STATE_DTYPE:
+        return np.ascontiguousarray(states)
+    a = np.zeros(len(states), C4_STATE_DTYPE)
+    for i, s in enumerate(states):
+        a[i]["x"], a[i]["o"], a[i]["n"], a[i]["status"] = s[0], s[1], s[2], s[3]
+    return a
+
+
+class Net:
+    """Net (model/mod.rs:22-28) on the device; Model::predict as .predict()."""
+
+    def __init__(self, engine, blocks, params, hidden=64):
+        params = np.ascontiguousarray(params, np.float32)
+        self.engine, self.blocks, self.hidden = engine, blocks, hidden
+        h = C.c_void_p()
+        _check(lib().spai_net_create(engine.h, blocks, hidden, _p(params), params.size, C.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().spai_net_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def forward(self, x):
+        x = np.ascontiguousarray(x, np.float32).reshape(-1, 126)
+        n = x.shape[0]
+        lg = np.zeros((n, 7), np.float32)
+        v = np.zeros(n, np.float32)
+        _check(lib().spai_net_forward(self.h, n, _p(x), _p(lg), _p(v)))
+        return lg, v
+
+    def predict(self, states):
+        a = states_array(states)
+        n = len(a)
+        pr = np.zeros((n, 7), np.float32)
+        v = np.zeros(n, np.float32)
+        _check(lib().spai_predict(self.h, n, _p(a), _p(pr), _p(v)))
+        return pr, v
+
+
+class Engine:
+    def __init__(self, num_searches=800, max_trees=4096, eval_kind=EVAL_NET, device=0, c=2.0, temperature=1.25,
+                 seed=0, max_moves=42, game=GAME_CONNECT4):
+        cfg = Config()
+        _check(lib().spai_config_default(game, C.byref(cfg)))
+        cfg.c, cfg.num_searches, cfg.temperature = c, num_searches, temperature
+        cfg.max_trees, cfg.max_moves, cfg.eval, cfg.seed = max_trees, max_moves, eval_kind, seed
+        self.cfg = cfg
+        h = C.c_void_p()
+        _check(lib().spai_engine_create(game, C.byref(cfg), device, C.byref(h)))
+        self.h = h
+        self.net = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            if self.net is not None:
+                self.net.close()
+                self.net = None
+            lib().spai_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def sync(self):
+        _check(lib().spai_engine_sync(self.h))
+
+    # ---- rules
+    def games_resize(self, n):
+        _check(lib().spai_games_resize(self.h, n))
+
+    def games_write(self, states, first=0):
+        a = states_array(states)
+        _check(lib().spai_games_write(self.h, first, len(a), _p(a)))
+
+    def games_read(self, n, first=0):
+        a = np.zeros(n, C4_STATE_DTYPE)
+        _check(lib().spai_games_read(self.h, first, n, _p(a)))
+        return a
+
+    def legal_mask(self, n, first=0):
+        m = np.zeros(n, np.uint32)
+        _check(lib().spai_legal_mask(self.h, first, n, _p(m)))
+        return m
+
+    def apply(self, actions, first=0, check=True):
+        a = np.ascontiguousarray(actions, np.int32)
+        rc = np.zeros(len(a), np.int32)
+        r = lib().spai_apply(self.h, first, len(a), _p(a), _p(rc))
+        if check:
+            _check(r)
+        return rc
+
+    def value_terminated(self, n, first=0):
+        v = np.zeros(n, np.float32)
+        t = np.zeros(n, np.uint8)
+        _check(lib().spai_value_terminated(self.h, first, n, _p(v), _p(t)))
+        return v, t
+
+    def encode(self, n, first=0):
+        e = np.zeros((n, 3, 6, 7), np.float32)
+        _check(lib().spai_encode(self.h, first, n, _p(e)))
+        return e
+
+    def mask_invalid(self, policy, first=0):
+        p = np.ascontiguousarray(policy, np.float32)
+        n, ln = p.shape
+        out = np.zeros((n, 7), np.float32)
+        _check(lib().spai_mask_invalid(self.h, first, n, _p(p), ln, _p(out)))
+        return out
+
+    def rules_bench(self, n, iters=20):
+        ms = np.zeros(3, np.float64)
+        _check(lib().spai_rules_bench(self.h, n, iters, _p(ms)))
+        return ms
+
+    # ---- net
+    def set_net(self, net):
+        _check(lib().spai_engine_set_net(self.h, net.h if net is not None else None))
+        self.net = net
+
+    # ---- search
+    def trees_create(self, n):
+        _check(lib().spai_trees_create(self.h, n))
+
+    def tree_reset(self, t, root=None):
+        if root is None:
+            _check(lib().spai_tree_reset(self.h, t, None))
+        else:
+            a = states_array([root])
+            _check(lib().spai_tree_reset(self.h, t, _p(a)))
+
+    def search(self, tree_idx, num_searches=None):
+        idx = np.ascontiguousarray(tree_idx, np.uint32)
+        n = len(idx)
+        ns = self.cfg.num_searches if num_searches is None else num_searches
+        pol = np.zeros((n, 7), np.float32)
+        ids = np.zeros((n, 7), np.uint32)
+        vis = np.zeros((n, 7), np.float32)
+        nc = np.zeros(n, np.uint32)
+        _check(lib().spai_search(self.h, n, _p(idx), ns, _p(pol), _p(ids), _p(vis), _p(nc)))
+        return pol, ids, vis, nc
+
+    def use_subtree(self, t, child_id):
+        _check(lib().spai_tree_use_subtree(self.h, t, int(child_id)))
+
+    def tree_node(self, t, node):
+        a = np.zeros(1, C4_STATE_DTYPE)
+        vis = C.c_uint32()
+        w = C.c_float()
+        _check(lib().spai_tree_node(self.h, t, int(node), _p(a), C.byref(vis), C.byref(w)))
+        return a[0], vis.value, w.value
+
+    def tree_size(self, t):
+        n = C.c_uint32()
+        _check(lib().spai_tree_size(self.h, t, C.byref(n)))
+        return n.value
+
+    # ---- self-play
+    def self_play(self, n_games, game_id_base=0, collect=True):
+        games = []
+
+        def sink(user, gid, n, enc, pol, val, moves):
+            if collect:
+                games.append(dict(game=gid,
+                                  enc=np.ctypeslib.as_array(enc, (n, 126)).copy(),
+                                  policy=np.ctypeslib.as_array(pol, (n, 7)).copy(),
+                                  value=np.ctypeslib.as_array(val, (n,)).copy(),
+                                  moves=np.ctypeslib.as_array(moves, (n,)).copy()))
+
+        cb = SINK(sink)
+        st = SelfPlayStats()
+        _check(lib().spai_selfplay_run(self.h, n_games, game_id_base, cb, None, C.byref(st)))
+        return games, {k: getattr(st, k) for k, _ in SelfPlayStats._fields_}
+
+    # ---- profiling
+    def set_timing(self, on):
+        _check(lib().spai_engine_set_timing(self.h, int(bool(on))))
+
+    def timing(self):
+        avg = np.zeros(3, np.float64)
+        launches = np.zeros(3, np.float64)
+        tot = np.zeros(3, np.float64)
+        items = np.zeros(3, np.float64)
+        _check(lib().spai_engine_timing(self.h, _p(avg), _p(launches)))
+        _check(lib().spai_engine_timing_items(self.h, _p(tot), _p(items)))
+        names = ("select", "evaluate", "expand")
+        return {nm: dict(avg_ms=avg[i], launches=launches[i], total_ms=tot[i], items=items[i])
+                for i, nm in enumerate(names)}

@@ -1,0 +1,319 @@
+"""GPU parity tests: the HIP path (libspai.so via its C ABI) against the CPU
+oracle and the golden fixtures.  Run on the MI355X box: pytest -m gpu.
+
+Bars: rules, search and self-play with the deterministic stub evaluators are
+bit-exact; the bf16 net is compared with libtorch fp32 / the fp32 oracle at the
+tolerances stated in each test.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def spai():
+    import spai as s
+    assert s.device_count() > 0, "no GPU visible"
+    return s
+
+
+@pytest.fixture(scope="module")
+def eng(spai):
+    e = spai.Engine(num_searches=64, max_trees=512, eval_kind=spai.EVAL_HASH, seed=7)
+    yield e
+    e.close()
+
+
+def _random_games(n, plies, seed):
+    """random action sequences (may contain illegal moves, which must be reported)"""
+    rng = np.random.default_rng(seed)
+    return rng.integers(0, 7, size=(n, plies)).astype(np.int32)
+
+
+# ------------------------------------------------------------------ rules
+def test_rules_lockstep_random_games(spai, oracle):
+    """1M+ positions: play 32768 random legal games in lockstep on the GPU and
+    compare every ply's legal mask / status / bitboards with the oracle."""
+    n, P = 32768, 42
+    e = spai.Engine(num_searches=1, max_trees=1, eval_kind=spai.EVAL_HASH)
+    e.games_resize(n)
+    rng = np.random.default_rng(0)
+    acts = np.full((n, P), -1, np.int32)
+    legal_hist, status_hist, x_hist, o_hist = [], [], [], []
+    alive = np.ones(n, bool)
+    for p in range(P + 1):
+        lm = e.legal_mask(n)
+        st = e.games_read(n)
+        v, t = e.value_terminated(n)
+        legal_hist.append(lm)
+        status_hist.append(st["status"].copy())
+        x_hist.append(st["x"].copy())
+        o_hist.append(st["o"].copy())
+        assert np.array_equal(t.astype(bool), st["status"] != 0)
+        assert np.all(v[st["status"] == spai.WON] == -1.0) and np.all(v[st["status"] != spai.WON] == 0.0)
+        if p == P:
+            break
+        alive &= lm != 0
+        # pick a random legal column per live game
+        r = rng.random((n, 7)) * ((lm[:, None] >> np.arange(7)) & 1)
+        a = np.where(alive, np.argmax(r, axis=1), 0).astype(np.int32)
+        acts[alive, p] = a[alive]
+        rc = e.apply(a, check=False)
+        assert np.all(rc[alive] == 0)
+        assert np.all(rc[~alive] == -3)  # Game has already ended
+    ref = oracle.c4_replay(acts)
+    for p in range(P + 1):
+        live = np.array([True] * n)
+        np.testing.assert_array_equal(legal_hist[p][live], ref["legal"][:, p][live])
+        np.testing.assert_array_equal(status_hist[p], ref["status"][:, p])
+        np.testing.assert_array_equal(x_hist[p], ref["x"][:, p])
+        np.testing.assert_array_equal(o_hist[p], ref["o"][:, p])
+    e.close()
+
+
+def test_rules_encode_mask_and_errors(spai, oracle):
+    with open(os.path.join(GOLDEN, "rules_c4.json")) as f:
+        traces = json.load(f)["traces"]
+    states, refs = [], []
+    for g in traces[:80]:
+        for p in g["plies"]:
+            states.append((int(p["x"]), int(p["o"]), p["n"], p["status"]))
+            refs.append(p)
+    n = len(states)
+    e = spai.Engine(num_searches=1, max_trees=1, eval_kind=spai.EVAL_HASH)
+    e.games_resize(n)
+    e.games_write(states)
+    enc = e.encode(n)
+    lm = e.legal_mask(n)
+    for i, p in enumerate(refs):
+        assert float(enc[i].ravel() @ np.arange(126)) == p["enc_sum"]
+        assert lm[i] == p["legal"]
+    rng = np.random.default_rng(1)
+    pol = rng.random((n, 7)).astype(np.float32)
+    got = e.mask_invalid(pol)
+    for i, (x, o, nn, st) in enumerate(states[:300]):
+        s = _oracle_state(oracle, x, o, nn, st)
+        if st == 0:
+            np.testing.assert_array_equal(got[i], s.mask_invalid(pol[i]))
+    with pytest.raises(spai.SpaiError):
+        e.mask_invalid(np.ones((n, 6), np.float32))
+    # full column -> ILLEGAL_MOVE, slot unchanged
+    e.games_resize(1)
+    for _ in range(6):
+        e.apply([3])
+    before = e.games_read(1)
+    rc = e.apply([3], check=False)
+    assert rc[0] == -2
+    assert e.games_read(1).tobytes() == before.tobytes()
+    # out-of-range action -> INVALID
+    assert e.apply([7], check=False)[0] == -1
+    e.close()
+
+
+def test_rules_kernels_bench_runs(spai):
+    e = spai.Engine(num_searches=1, max_trees=1)
+    ms = e.rules_bench(1 << 20, iters=3)
+    assert np.all(ms > 0)
+    e.close()
+
+
+# ------------------------------------------------------------------ net
+BF16_TOL = dict(rtol=3e-2, atol=3e-2)   # bf16 weights/activations, fp32 accumulate
+
+
+def test_net_forward_vs_libtorch_golden(spai):
+    z = np.load(os.path.join(GOLDEN, "net_c4_2x64.npz"))
+    blocks, hidden, seed = [int(v) for v in z["meta"]]
+    e = spai.Engine(num_searches=1, max_trees=1)
+    net = spai.Net(e, blocks, z["params"])
+    lg, v = net.forward(z["x"])
+    scale = np.abs(z["logits"]).max()
+    assert np.abs(lg - z["logits"]).max() <= 3e-2 * max(1.0, scale), np.abs(lg - z["logits"]).max()
+    np.testing.assert_allclose(v, z["value"], **BF16_TOL)
+    # Model::predict: softmax -> mask -> renormalise (model/mod.rs:62-93)
+    b = z["boards"]
+    states = [(int(b[i, 0]), int(b[i, 1]), int(b[i, 2]), 0) for i in range(len(b))]
+    pr, pv = net.predict(states)
+    np.testing.assert_allclose(pr, z["priors"], rtol=0, atol=2e-2)
+    np.testing.assert_allclose(pr.sum(1), 1.0, atol=1e-5)
+    np.testing.assert_allclose(pv, z["value"], **BF16_TOL)
+    legal = np.array([[(~(x | o) >> (7 * a + 5)) & 1 for a in range(7)] for x, o, _, _ in states])
+    assert np.all(pr[legal == 0] == 0.0)
+    net.close()
+    e.close()
+
+
+def test_net_6x64_vs_oracle_fp32(spai, oracle):
+    p = spai.init_params(6, 64, seed=0)
+    np.testing.assert_array_equal(p, oracle.init_params(1, 6, 64, 0))  # same init stream
+    e = spai.Engine(num_searches=1, max_trees=1)
+    net = spai.Net(e, 6, p)
+    rng = np.random.default_rng(3)
+    acts = rng.integers(0, 7, size=(48, 20)).astype(np.int32)
+    ref = oracle.c4_replay(acts)
+    xs = []
+    for g in range(48):
+        for ply in (0, 5, 11, 19):
+            if ref["status"][g, ply] == 0:
+                xs.append(_oracle_state(oracle, int(ref["x"][g, ply]), int(ref["o"][g, ply]), ply, 0).encoding())
+    x = np.stack(xs)
+    on = oracle.Net(1, 6, 64, p)
+    rl, rv = on.forward(x)
+    lg, v = net.forward(x)
+    err = np.abs(lg - rl).max() / max(1.0, np.abs(rl).max())
+    assert err < 3e-2, err
+    np.testing.assert_allclose(v, rv, rtol=5e-2, atol=5e-2)
+    net.close()
+    e.close()
+
+
+def test_net_partial_batches(spai):
+    """batch sizes that are not multiples of the 8-position workgroup tile"""
+    z = np.load(os.path.join(GOLDEN, "net_c4_2x64.npz"))
+    e = spai.Engine(num_searches=1, max_trees=1)
+    net = spai.Net(e, 2, z["params"])
+    full_l, full_v = net.forward(z["x"])
+    for n in (1, 3, 8, 9, 17, 255):
+        lg, v = net.forward(z["x"][:n])
+        np.testing.assert_array_equal(lg, full_l[:n])   # per-position results are batch independent
+        np.testing.assert_array_equal(v, full_v[:n])
+    net.close()
+    e.close()
+
+
+# ------------------------------------------------------------------ search
+def test_search_hash_matches_oracle(spai, oracle, eng):
+    d = json.load(open(os.path.join(GOLDEN, "mcts_hash.json")))
+    cases = d["search"]
+    eng.trees_create(len(cases))
+    for i, c in enumerate(cases):
+        eng.tree_reset(i, (int(c["x"]), int(c["o"]), c["n"], 0))
+    for i, c in enumerate(cases):
+        pol, ids, vis, nc = eng.search([i], c["sims"])
+        assert [int(v) for v in vis[0, :nc[0]]] == c["visits"], (i, c)
+        np.testing.assert_array_equal(pol[0], np.array(c["policy"], np.float32))
+
+
+def test_search_uniform_first_select(spai):
+    e = spai.Engine(num_searches=2, max_trees=4, eval_kind=spai.EVAL_UNIFORM)
+    e.trees_create(1)
+    pol, ids, vis, nc = e.search([0], 2)
+    assert list(vis[0, :nc[0]]) == [0, 0, 0, 0, 0, 0, 1]   # ties -> last child (column 6)
+    e.close()
+
+
+def test_search_batched_with_subtree_reuse(spai, oracle):
+    """many trees searched together, then re-rooted (use_subtree keeps N, W) and searched again"""
+    n, sims = 96, 48
+    rng = np.random.default_rng(5)
+    roots = []
+    for g in range(n):
+        s = oracle.C4()
+        for _ in range(int(rng.integers(0, 14))):
+            va = s.valid_actions()
+            if not va:
+                break
+            nx = s.next_state(int(rng.choice(va)))
+            if nx.status != 0:
+                break
+            s = nx
+        roots.append(s)
+    e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_HASH, max_moves=4)
+    e.trees_create(n)
+    for i, s in enumerate(roots):
+        x, o = s.bitboards()
+        e.tree_reset(i, (x, o, s.n, 0))
+    L = oracle.lib()
+    trees = [L.or_tree_with_root(oracle.GAME_CONNECT4, oracle.C.byref(s.st)) for s in roots]
+    for rnd in range(3):
+        idx = np.arange(n)
+        pol, ids, vis, nc = e.search(idx, sims)
+        rc, rp, rids, rvis, rnc = oracle.search_c4(None, sims, trees=trees)
+        np.testing.assert_array_equal(nc, rnc)
+        np.testing.assert_array_equal(vis, rvis)
+        np.testing.assert_array_equal(pol, rp)
+        # re-root on the most visited non-terminal child (last max)
+        for i in range(n):
+            k = int(nc[i])
+            if k == 0:
+                continue
+            j = int(np.flatnonzero(vis[i, :k] == vis[i, :k].max())[-1])
+            st = oracle.C4(oracle.C4State.from_buffer_copy(
+                oracle.C.string_at(L.or_tree_node_state(trees[i], int(rids[i, j])), oracle.C.sizeof(oracle.C4State))))
+            if st.status != 0:
+                continue
+            e.use_subtree(i, ids[i, j])
+            L.or_tree_use_subtree(trees[i], int(rids[i, j]))
+            gs, gvis, gw = e.tree_node(i, ids[i, j])
+            x, o = st.bitboards()
+            assert (int(gs["x"]), int(gs["o"]), int(gs["n"])) == (x, o, st.n)
+    for t in trees:
+        L.or_tree_destroy(t)
+    e.close()
+
+
+# ------------------------------------------------------------------ self-play
+def test_self_play_hash_matches_oracle(spai, oracle):
+    n, sims, seed = 64, 32, 11
+    e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_HASH, seed=seed)
+    games, stats = e.self_play(n)
+    ref = oracle.self_play(oracle.GAME_CONNECT4, n, sims, seed, eval_kind=oracle.EVAL_HASH, max_plies=42)
+    # same emission order: game by game as the reference removes finished trees
+    k = 0
+    for g in games:
+        m = len(g["value"])
+        assert list(ref["game"][k:k + m]) == [g["game"]] * m
+        np.testing.assert_array_equal(g["policy"], ref["policy"][k:k + m])
+        np.testing.assert_array_equal(g["value"], ref["value"][k:k + m])
+        np.testing.assert_array_equal(g["enc"], ref["enc"][k:k + m])
+        assert list(g["moves"]) == list(ref["moves"][g["game"], :m])
+        k += m
+    assert k == len(ref["value"])
+    assert stats["games"] == n and stats["sims"] == ref["sims"]
+    e.close()
+
+
+def test_self_play_net_properties(spai, oracle):
+    """bf16 net self-play: every game is a legal Connect4 game ending in the
+    recorded outcome; values are +-1/0 by perspective; policies are normalised."""
+    n, sims = 128, 16
+    e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_NET, seed=3)
+    net = spai.Net(e, 6, spai.init_params(6, 64, seed=1))
+    e.set_net(net)
+    games, stats = e.self_play(n)
+    assert len(games) == n and stats["games"] == n
+    for g in games:
+        mv = g["moves"]
+        s = oracle.C4()
+        for a in mv:
+            s = s.next_state(int(a))
+        assert s.status != 0
+        m = len(mv)
+        last = 1.0 if s.status == 2 else 0.0
+        # the player who made the last move won: positions where they were to move get +1
+        exp = np.array([last if (m - 1 - i) % 2 == 0 else -last for i in range(m)], np.float32)
+        np.testing.assert_array_equal(g["value"], exp)
+        np.testing.assert_allclose(g["policy"].sum(1), 1.0, atol=1e-6)
+    e.close()
+
+
+def _oracle_state(oracle, x, o, n, status):
+    st = oracle.C4State()
+    oracle.lib().or_c4_init(oracle.C.byref(st))
+    for col in range(7):
+        for row in range(6):
+            b = 1 << (col * 7 + row)
+            if x & b:
+                st.board[row][col] = oracle.X
+            elif o & b:
+                st.board[row][col] = oracle.O
+    st.num_actions_played = n
+    st.current_player = oracle.X if n % 2 == 0 else oracle.O
+    st.status = status
+    return oracle.C4(st)
