@@ -154,10 +154,12 @@ long or_c4_replay(int n, int max_plies, const int32_t *actions, uint32_t *legal,
                   uint64_t *os, int32_t *rc) {
     long total = 0;
     for (int g = 0; g < n; ++g) {
+        const size_t base = (size_t)g * (max_plies + 1);
         or_c4_state s;
         or_c4_init(&s);
-        for (int p = 0; p <= max_plies; ++p) {
-            size_t k = (size_t)g * (max_plies + 1) + p;
+        int p = 0;
+        for (;; ++p) {
+            const size_t k = base + p;
             int acts[7];
             int na = or_c4_valid_actions(&s, acts);
             uint32_t m = 0;
@@ -174,6 +176,14 @@ long or_c4_replay(int n, int max_plies, const int32_t *actions, uint32_t *legal,
             if (rc[k] != 0) break;
             s = nx;
             ++total;
+        }
+        for (int q = p + 1; q <= max_plies; ++q) {   /* later plies keep the final state */
+            const size_t k = base + q, l = base + p;
+            legal[k] = legal[l];
+            status[k] = status[l];
+            xs[k] = xs[l];
+            os[k] = os[l];
+            rc[k] = 0;
         }
     }
     return total;
