@@ -354,6 +354,13 @@ int spai_engine_timing(spai_engine *e, double *avg_ms, double *launches) {
     return SPAI_OK;
 }
 
+int spai_net_phase_cycles(spai_net *n, uint32_t count, double *cycles) {
+    PTR_CHECK(n);
+    PTR_CHECK(cycles);
+    ENG_CHECK(n->eng);
+    return net_phase_stamps(n, count, cycles);
+}
+
 int spai_engine_timing_items(spai_engine *e, double *total_ms, double *items) {
     ENG_CHECK(e);
     for (int i = 0; i < 3; ++i) {

@@ -21,9 +21,9 @@
 //    leaf bitboards (encoding fused, connect_four.rs:242-259).
 //  * epilogues fuse bias, residual add and ReLU; the head conv writes fp32,
 //    the two linears, tanh, softmax and the legal-move mask run in-kernel.
-//  * wave w owns position tiles [6,5,5,5] of the 21 16-position tiles and all
-//    4 co tiles (24/20 accumulators).
+//  * wave W owns 21 of the 84 (position tile, co tile) tasks of a 64-channel layer
 // Algorithmic FLOPs per position (6 blocks x 64): 39,016,572.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 
@@ -38,7 +38,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kHid = 64;
 constexpr int kS = 8;                      // positions per workgroup
 constexpr int kP = kS * c4::kCells;        // 336 board cells per workgroup
-constexpr int kPT = kP / 16;               // 21 position tiles
 constexpr int kWaves = 4;
 constexpr int kThreads = kWaves * 64;
 constexpr int kKStepsRes = 18;             // 576 / 32
@@ -48,14 +47,22 @@ constexpr int kPolIn = 32 * c4::kCells;    // 1344
 constexpr int kValIn = 3 * c4::kCells;     // 126
 
 // LDS carve (bytes)
-constexpr int kZ = 0;                      // 128 B of zeros (out-of-board taps)
+constexpr int kZ = 0;                      // 128 B of zeros: row -1 of X
 constexpr int kX = 128;                    // [336][128 B] bf16 activations
-constexpr int kY = kX + kP * 128;          // second activation buffer
+constexpr int kZ1 = kX + kP * 128;         // 128 B of zeros: row -1 of Y
+constexpr int kY = kZ1 + 128;              // second activation buffer
 constexpr int kH = kY;                     // fp32 head conv output [8][35][42] overlays Y
 constexpr int kHBytes = kS * kHeadC * c4::kCells * 4;
 constexpr int kB = kH + kHBytes;           // 8 x (mine, theirs)
 constexpr int kL = kB + kS * 16;           // logits scratch [8][8] f32
-constexpr int kLdsBytes = kL + kS * 8 * 4;
+constexpr int kMaxBlocks = 20;
+constexpr int kBiasFloats = kHid + 2 * kMaxBlocks * kHid + 48;   // stem, residual convs, head
+constexpr int kBias = kL + kS * 8 * 4;     // all conv biases, staged once per workgroup
+constexpr int kPlanes = kBias + kBiasFloats * 4;   // stem neighbour planes [8][32] u64
+constexpr int kLinFloats = 9728;           // policy [7][1344] + value [126] + pad to 38 KiB
+constexpr int kLin = kPlanes + kS * 32 * 8;        // head linear weights (LDS-DMA at kernel start)
+constexpr int kLdsBytes = kLin + kLinFloats * 4;
+constexpr int kStamps = 17;                // phase stamps per wave in the diagnostic mode
 static_assert(kY + kP * 128 <= kB, "heads overlay");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 
@@ -66,12 +73,16 @@ struct NetParams {
     const float *b_stem;   // [64]
     const float *b_res;    // [2*blocks][64]
     const float *b_head;   // [48]
-    const float *w_pol;    // [7][1344]
+    const float *w_lin;    // [7][1344] policy | [126] value | zero pad, kLinFloats
     const float *b_pol;    // [7]
-    const float *w_val;    // [126]
     const float *b_val;    // [1]
+    unsigned long long *stamps;   // diagnostic: [grid][4 waves][kStamps] s_memtime, or null
     int blocks;
 };
+
+__device__ __forceinline__ void stamp(const NetParams &P, int wave, int lane, int k) {
+    if (P.stamps && lane == 0) P.stamps[((size_t)blockIdx.x * kWaves + wave) * kStamps + k] = __builtin_amdgcn_s_memtime();
+}
 
 __device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
 
@@ -80,182 +91,260 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
     return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
 }
 
-// byte offset of the 16-B channel chunk `c` (0..7) of activation row `r` in a buffer at `base`
-__device__ __forceinline__ int act_off(int base, int r, int c) { return base + r * 128 + ((c ^ (r & 7)) << 4); }
+// Work split: a conv layer is 21 position tiles x CT co tiles = 21*CT tile-tasks
+// (task = pos_tile*CT + co_tile).  Wave W owns tasks [TT*W/4, TT*(W+1)/4): 21
+// each for the 64-channel layers, so all four SIMDs issue the same MFMA count.
+template <int W, int CT>
+struct Plan {
+    static constexpr int TT = 21 * CT;
+    static constexpr int first = TT * W / 4;
+    static constexpr int n = TT * (W + 1) / 4 - first;      // tasks of this wave
+    static constexpr int T0 = first / CT;                   // first position tile touched
+    static constexpr int NT = (first + n - 1) / CT - T0 + 1;  // position tiles touched (<= 6)
+    static constexpr int pt(int i) { return (first + i) / CT - T0; }
+    static constexpr int co(int i) { return (first + i) % CT; }
+};
 
-// implicit-GEMM 3x3 conv over LDS activations at `in_base`: acc[t][ct] += W[ct] * X[tile t]
-template <int NT, int CT>
-__device__ __forceinline__ void conv_mfma(const uint8_t *smem, int in_base, const uint4 *__restrict__ w, int t0,
-                                          int lane, f32x4 (&acc)[NT][CT]) {
-    const int col = lane & 15, q = lane >> 4;
-    int pos[NT], ph[NT], pw[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-        int p = (t0 + t) * 16 + col;
-        int cell = p % c4::kCells;
-        pos[t] = p;
-        ph[t] = cell / c4::kCols;
-        pw[t] = cell - ph[t] * c4::kCols;
-    }
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int c = 0; c < CT; ++c) acc[t][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    uint4 a_cur[2][CT];
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-        for (int c = 0; c < CT; ++c) a_cur[hf][c] = w[(hf * CT + c) * 64 + lane];
-
-#pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-        const int dh = tap / 3 - 1, dw = tap % 3 - 1;
-        uint4 a_nxt[2][CT];
-        if (tap < 8) {
-#pragma unroll
-            for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-                for (int c = 0; c < CT; ++c) a_nxt[hf][c] = w[(((tap + 1) * 2 + hf) * CT + c) * 64 + lane];
-        }
-        int rows[NT];
-        bool ok[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            ok[t] = (unsigned)(ph[t] + dh) < (unsigned)c4::kRows && (unsigned)(pw[t] + dw) < (unsigned)c4::kCols;
-            rows[t] = pos[t] + dh * c4::kCols + dw;
-        }
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-            uint4 b[NT];
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                int off = ok[t] ? act_off(in_base, rows[t], hf * 4 + q) : kZ + (q << 4);
-                b[t] = *(const uint4 *)(smem + off);
-            }
-#pragma unroll
-            for (int t = 0; t < NT; ++t)
-#pragma unroll
-                for (int c = 0; c < CT; ++c)
-                    acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a_cur[hf][c]), as_bf16x8(b[t]),
-                                                                       acc[t][c], 0, 0, 0);
-        }
-        if (tap < 8) {
-#pragma unroll
-            for (int hf = 0; hf < 2; ++hf)
-#pragma unroll
-                for (int c = 0; c < CT; ++c) a_cur[hf][c] = a_nxt[hf][c];
-        }
-    }
-}
-
-// epilogue for a 64-channel bf16 output: relu(acc + bias [+ residual]) -> LDS
+// Per-lane LDS geometry, computed once per kernel (positions are the same for
+// every layer).  For tile t and tap (dh,dw) the B-fragment address relative to
+// the activation buffer is rel[t][tap] (k-step half 0; half 1 = rel ^ 64, the
+// swizzled chunk index flips bit 2).  An out-of-board tap points at row -1 of
+// the buffer, a zeroed 128-B row, so the k-loop needs no select.  epi[t] is the
+// relative address of this lane's 4 output channels of co tile 0 at its
+// position (co tile c: epi ^ (c << 5)).
 template <int NT>
-__device__ __forceinline__ void epilogue_act(uint8_t *smem, int out_base, const float *__restrict__ bias, int t0,
-                                             int lane, bool residual, f32x4 (&acc)[NT][4]) {
+struct Geo {
+    int rel[NT][9];
+    int epi[NT];
+};
+
+template <int W, int CT>
+__device__ __forceinline__ void make_geo(int lane, Geo<Plan<W, CT>::NT> &g) {
+    using PL = Plan<W, CT>;
     const int col = lane & 15, q = lane >> 4;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const int co0 = c * 16 + 4 * q;
-        const float4 b = *(const float4 *)(bias + co0);
+    for (int t = 0; t < PL::NT; ++t) {
+        const int p = (PL::T0 + t) * 16 + col;
+        const int cell = p % c4::kCells;
+        const int h = cell / c4::kCols, w = cell - h * c4::kCols;
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int p = (t0 + t) * 16 + col;
-            const int off = act_off(out_base, p, co0 >> 3) + ((co0 & 4) << 1);
-            float v0 = acc[t][c][0] + b.x, v1 = acc[t][c][1] + b.y, v2 = acc[t][c][2] + b.z, v3 = acc[t][c][3] + b.w;
-            if (residual) {
-                uint2 r = *(const uint2 *)(smem + off);
-                v0 += __builtin_bit_cast(float, r.x << 16);
-                v1 += __builtin_bit_cast(float, r.x & 0xFFFF0000u);
-                v2 += __builtin_bit_cast(float, r.y << 16);
-                v3 += __builtin_bit_cast(float, r.y & 0xFFFF0000u);
-            }
-            v0 = fmaxf(v0, 0.f);
-            v1 = fmaxf(v1, 0.f);
-            v2 = fmaxf(v2, 0.f);
-            v3 = fmaxf(v3, 0.f);
-            *(uint2 *)(smem + off) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+        for (int tap = 0; tap < 9; ++tap) {
+            const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+            const int r = p + dh * c4::kCols + dw;
+            const bool ok = (unsigned)(h + dh) < (unsigned)c4::kRows && (unsigned)(w + dw) < (unsigned)c4::kCols;
+            g.rel[t][tap] = ok ? r * 128 + ((q ^ (r & 7)) << 4) : -128 + (q << 4);
         }
+        g.epi[t] = p * 128 + ((((q >> 1)) ^ (p & 7)) << 4) + ((q & 1) << 3);
     }
 }
 
-// stem: B operand = the 27 input planes x taps built in registers, one k-step
-template <int NT, bool FROM_X>
+// implicit-GEMM 3x3 conv over the LDS activations at IN for wave W's tasks.
+// Software pipeline: A (weights, global/L2) two k-steps ahead, B (LDS) one
+// k-step ahead; sched_group_barrier interleaves the prefetch with the MFMAs
+// (and keeps the scheduler from sinking loads onto their uses).  The first
+// k-step takes the bias as its C operand, so the accumulators need no zeroing
+// and the epilogue no bias add.  The A ring is the caller's: A[0], A[1] arrive
+// holding k-steps 0 and 1, and the last two k-steps refill them with k-steps 0
+// and 1 of the next layer (`wn`, may be null), so consecutive layers stream
+// weights without a cold start.
+template <int W, int CT, int IN>
+__device__ __forceinline__ void conv_mfma(const uint8_t *smem, const Geo<Plan<W, CT>::NT> &g, const float *bias,
+                                          const uint4 *__restrict__ w, const uint4 *__restrict__ wn, int lane,
+                                          uint4 (&A)[3][CT], f32x4 (&acc)[Plan<W, CT>::n]) {
+    using PL = Plan<W, CT>;
+    constexpr int NT = PL::NT;
+    const int q = lane >> 4;
+    f32x4 bv[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        const float4 b = *(const float4 *)(bias + c * 16 + 4 * q);
+        bv[c] = f32x4{b.x, b.y, b.z, b.w};
+    }
+    const uint4 *wl = w + lane;
+    const uint4 *wnl = wn ? wn + lane : nullptr;
+    uint4 B[2][NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) B[0][t] = *(const uint4 *)(smem + IN + g.rel[t][0]);
+#pragma unroll
+    for (int ks = 0; ks < kKStepsRes; ++ks) {
+        if (ks + 2 < kKStepsRes) {
+#pragma unroll
+            for (int c = 0; c < CT; ++c) A[(ks + 2) % 3][c] = wl[((ks + 2) * CT + c) * 64];
+        } else if (wnl) {
+#pragma unroll
+            for (int c = 0; c < CT; ++c) A[(ks + 2) % 3][c] = wnl[((ks + 2 - kKStepsRes) * CT + c) * 64];
+        }
+        if (ks + 1 < kKStepsRes) {
+            const int tap = (ks + 1) >> 1, flip = ((ks + 1) & 1) << 6;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) B[(ks + 1) % 2][t] = *(const uint4 *)(smem + IN + (g.rel[t][tap] ^ flip));
+        }
+#pragma unroll
+        for (int i = 0; i < PL::n; ++i)
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[ks % 3][PL::co(i)]),
+                                                            as_bf16x8(B[ks % 2][PL::pt(i)]),
+                                                            ks == 0 ? bv[PL::co(i)] : acc[i], 0, 0, 0);
+        // issue order for this k-step: each MFMA followed by up to 2 VALU, one
+        // LDS read (next B) and one weight load (A, two ahead)
+#pragma unroll
+        for (int i = 0; i < PL::n; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+            if (i < NT) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            if (i < CT) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+template <int CT>
+__device__ __forceinline__ void load_a01(const uint4 *__restrict__ w, int lane, uint4 (&A)[3][CT]) {
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        A[0][c] = w[c * 64 + lane];
+        A[1][c] = w[(CT + c) * 64 + lane];
+    }
+}
+
+// epilogue for a 64-channel bf16 output: relu(acc [+ residual]) -> LDS at OUT
+template <int W, int OUT, bool RESIDUAL>
+__device__ __forceinline__ void epilogue_act(uint8_t *smem, const Geo<Plan<W, 4>::NT> &g, f32x4 (&acc)[Plan<W, 4>::n]) {
+    using PL = Plan<W, 4>;
+#pragma unroll
+    for (int i = 0; i < PL::n; ++i) {
+        const int off = OUT + (g.epi[PL::pt(i)] ^ (PL::co(i) << 5));
+        float v0 = acc[i][0], v1 = acc[i][1], v2 = acc[i][2], v3 = acc[i][3];
+        if (RESIDUAL) {
+            const uint2 r = *(const uint2 *)(smem + off);
+            v0 += __builtin_bit_cast(float, r.x << 16);
+            v1 += __builtin_bit_cast(float, r.x & 0xFFFF0000u);
+            v2 += __builtin_bit_cast(float, r.y << 16);
+            v3 += __builtin_bit_cast(float, r.y & 0xFFFF0000u);
+        }
+        v0 = fmaxf(v0, 0.f);
+        v1 = fmaxf(v1, 0.f);
+        v2 = fmaxf(v2, 0.f);
+        v3 = fmaxf(v3, 0.f);
+        *(uint2 *)(smem + off) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+    }
+}
+
+// stem: one k-step, k = tap*3 + plane (27 of 32 used).  Bitboard path: the
+// neighbour planes N[s][k] (one u64 per sample/tap/plane, built at kernel start)
+// hold at bit col*7+row the value of that cell's (dh,dw) neighbour, so lane
+// element j of a position is bit (col*7+row) of N[s][8q+j].  FROM_X path
+// (Net::forward on arbitrary inputs): gather the fp32 input tensor.
+template <int W, bool FROM_X>
 __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const float *__restrict__ x, int base_slot,
-                                     int valid, int t0, int lane) {
+                                     int valid, int lane) {
+    using PL = Plan<W, 4>;
+    constexpr int NT = PL::NT;
     const int col = lane & 15, q = lane >> 4;
-    const uint64_t *bb = (const uint64_t *)(smem + kB);
     uint4 a[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) a[c] = P.w_stem[c * 64 + lane];
-    f32x4 acc[NT][4];
+    uint4 bv[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        const int p = (t0 + t) * 16 + col;
+        const int p = (PL::T0 + t) * 16 + col;
         const int s = p / c4::kCells, cell = p - s * c4::kCells;
         const int h = cell / c4::kCols, wc = cell - h * c4::kCols;
-        const uint64_t mine = bb[2 * s], theirs = bb[2 * s + 1], occ = mine | theirs;
         uint16_t e[8];
+        if (!FROM_X) {
+            const uint4 *np = (const uint4 *)(smem + kPlanes) + s * 16 + q * 4;   // N[s][8q .. 8q+7]
+            const int b = wc * 7 + h;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int kk = 8 * q + j;
-            float v = 0.f;
-            if (kk < 27) {
-                const int tap = kk / 3, ch = kk - tap * 3;
-                const int hh = h + tap / 3 - 1, ww = wc + tap % 3 - 1;
-                if ((unsigned)hh < (unsigned)c4::kRows && (unsigned)ww < (unsigned)c4::kCols) {
-                    if (FROM_X) {
-                        v = (s < valid) ? x[((size_t)(base_slot + s) * 3 + ch) * c4::kCells + hh * c4::kCols + ww] : 0.f;
-                    } else {
-                        const int bit = ww * 7 + hh;
-                        const uint64_t src = ch == 0 ? mine : ch == 1 ? theirs : ~occ;
-                        v = (float)((src >> bit) & 1ull);
-                    }
-                }
+            for (int j2 = 0; j2 < 4; ++j2) {
+                const uint4 w4 = np[j2];
+                const uint64_t n0 = (uint64_t)w4.x | ((uint64_t)w4.y << 32), n1 = (uint64_t)w4.z | ((uint64_t)w4.w << 32);
+                e[2 * j2] = ((n0 >> b) & 1ull) ? 0x3F80u : 0u;
+                e[2 * j2 + 1] = ((n1 >> b) & 1ull) ? 0x3F80u : 0u;
             }
-            e[j] = __builtin_bit_cast(uint16_t, (__bf16)v);
-        }
-        uint4 bv = make_uint4(e[0] | (uint32_t)e[1] << 16, e[2] | (uint32_t)e[3] << 16, e[4] | (uint32_t)e[5] << 16,
-                              e[6] | (uint32_t)e[7] << 16);
+        } else {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            acc[t][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-            acc[t][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[c]), as_bf16x8(bv), acc[t][c], 0, 0, 0);
+            for (int j = 0; j < 8; ++j) {
+                const int kk = 8 * q + j;
+                float v = 0.f;
+                if (kk < 27) {
+                    const int tap = kk / 3, ch = kk - tap * 3;
+                    const int hh = h + tap / 3 - 1, ww = wc + tap % 3 - 1;
+                    if ((unsigned)hh < (unsigned)c4::kRows && (unsigned)ww < (unsigned)c4::kCols && s < valid)
+                        v = x[((size_t)(base_slot + s) * 3 + ch) * c4::kCells + hh * c4::kCols + ww];
+                }
+                e[j] = __builtin_bit_cast(uint16_t, (__bf16)v);
+            }
         }
+        bv[t] = make_uint4(e[0] | (uint32_t)e[1] << 16, e[2] | (uint32_t)e[3] << 16, e[4] | (uint32_t)e[5] << 16,
+                           e[6] | (uint32_t)e[7] << 16);
     }
-    epilogue_act<NT>(smem, kX, P.b_stem, t0, lane, false, acc);
+    const float *bias = (const float *)(smem + kBias);
+    f32x4 b4[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float4 b = *(const float4 *)(bias + c * 16 + 4 * q);
+        b4[c] = f32x4{b.x, b.y, b.z, b.w};
+    }
+    f32x4 acc[PL::n];
+#pragma unroll
+    for (int i = 0; i < PL::n; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[PL::co(i)]), as_bf16x8(bv[PL::pt(i)]),
+                                                        b4[PL::co(i)], 0, 0, 0);
+    Geo<NT> g;
+    make_geo<W, 4>(lane, g);
+    epilogue_act<W, kX, false>(smem, g, acc);
 }
 
-template <int NT>
-__device__ __forceinline__ void res_layer(uint8_t *smem, const NetParams &P, int layer, int t0, int lane) {
-    f32x4 acc[NT][4];
-    const bool second = layer & 1;   // conv1: X -> Y ; conv2: Y -> X with residual X
-    conv_mfma<NT, 4>(smem, second ? kY : kX, P.w_res + (size_t)layer * kKStepsRes * 4 * 64, t0, lane, acc);
-    epilogue_act<NT>(smem, second ? kX : kY, P.b_res + layer * kHid, t0, lane, second, acc);
-}
-
-template <int NT>
-__device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, int t0, int lane) {
-    f32x4 acc[NT][kHeadCT];
-    conv_mfma<NT, kHeadCT>(smem, kX, P.w_head, t0, lane, acc);
+template <int W>
+__device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, int lane) {
+    using PL = Plan<W, kHeadCT>;
+    Geo<PL::NT> g;
+    make_geo<W, kHeadCT>(lane, g);
+    f32x4 acc[PL::n];
+    uint4 A[3][kHeadCT];
+    load_a01<kHeadCT>(P.w_head, lane, A);
+    conv_mfma<W, kHeadCT, kX>(smem, g, (const float *)(smem + kBias) + kHid * (1 + 2 * P.blocks), P.w_head, nullptr,
+                              lane, A, acc);
     const int col = lane & 15, q = lane >> 4;
     float *H = (float *)(smem + kH);
 #pragma unroll
-    for (int c = 0; c < kHeadCT; ++c) {
-        const int co0 = c * 16 + 4 * q;
-        const float4 b = *(const float4 *)(P.b_head + co0);
-        const float bv[4] = {b.x, b.y, b.z, b.w};
+    for (int i = 0; i < PL::n; ++i) {
+        const int co0 = PL::co(i) * 16 + 4 * q;
+        const int p = (PL::T0 + PL::pt(i)) * 16 + col;
+        const int s = p / c4::kCells, cell = p - s * c4::kCells;
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int p = (t0 + t) * 16 + col;
-            const int s = p / c4::kCells, cell = p - s * c4::kCells;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int co = co0 + r;
-                if (co < kHeadC) H[(s * kHeadC + co) * c4::kCells + cell] = fmaxf(acc[t][c][r] + bv[r], 0.f);
-            }
+        for (int r = 0; r < 4; ++r) {
+            const int co = co0 + r;
+            if (co < kHeadC) H[(s * kHeadC + co) * c4::kCells + cell] = fmaxf(acc[i][r], 0.f);
         }
     }
+}
+
+template <int W, bool FROM_X>
+__device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &P, const float *__restrict__ x,
+                                                int base, int valid, int lane) {
+    constexpr size_t kLayer = (size_t)kKStepsRes * 4 * 64;
+    const float *bias = (const float *)(smem + kBias);
+    uint4 A[3][4];
+    if (P.blocks > 0) load_a01<4>(P.w_res, lane, A);
+    stem<W, FROM_X>(smem, P, x, base, valid, lane);
+    Geo<Plan<W, 4>::NT> g;
+    make_geo<W, 4>(lane, g);
+    __syncthreads();
+    stamp(P, W, lane, 1);
+    for (int b = 0; b < P.blocks; ++b) {   // relu(x + BN(conv(relu(BN(conv(x)))))), model/mod.rs:152-165
+        f32x4 acc[Plan<W, 4>::n];
+        const int l1 = 2 * b, l2 = 2 * b + 1;
+        conv_mfma<W, 4, kX>(smem, g, bias + kHid * (1 + l1), P.w_res + l1 * kLayer, P.w_res + l2 * kLayer, lane, A, acc);
+        epilogue_act<W, kY, false>(smem, g, acc);
+        __syncthreads();
+        if (l1 < 12) stamp(P, W, lane, 2 + l1);
+        conv_mfma<W, 4, kY>(smem, g, bias + kHid * (1 + l2), P.w_res + l2 * kLayer,
+                            b + 1 < P.blocks ? P.w_res + (l2 + 1) * kLayer : nullptr, lane, A, acc);
+        epilogue_act<W, kX, true>(smem, g, acc);
+        __syncthreads();
+        if (l2 < 12) stamp(P, W, lane, 2 + l2);
+    }
+    head_layer<W>(smem, P, lane);
 }
 
 template <bool FROM_X>
@@ -272,6 +361,7 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
     if (tid < 32) ((uint32_t *)(smem + kZ))[tid] = 0u;
+    else if (tid < 64) ((uint32_t *)(smem + kZ1))[tid - 32] = 0u;
     if (tid < kS) {
         uint64_t m = 0, t = 0;
         if (!FROM_X && tid < valid) {
@@ -281,41 +371,71 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
         ((uint64_t *)(smem + kB))[2 * tid] = m;
         ((uint64_t *)(smem + kB))[2 * tid + 1] = t;
     }
-    __syncthreads();
-
-    // position tiles per wave: [0,6) [6,11) [11,16) [16,21)
-    const int t0 = wave == 0 ? 0 : 1 + 5 * wave;
-    if (wave == 0) stem<6, FROM_X>(smem, P, x, base, valid, t0, lane);
-    else stem<5, FROM_X>(smem, P, x, base, valid, t0, lane);
-    __syncthreads();
-    for (int layer = 0; layer < 2 * P.blocks; ++layer) {
-        if (wave == 0) res_layer<6>(smem, P, layer, t0, lane);
-        else res_layer<5>(smem, P, layer, t0, lane);
-        __syncthreads();
+    if (!FROM_X) {   // neighbour planes N[s][k]: k = tap*3 + plane, shifted so bit b = value at b's neighbour
+        const int s = tid >> 5, k = tid & 31;
+        uint64_t v = 0;
+        if (k < 27 && s < valid) {
+            const uint64_t m = mine[base + s], t = theirs[base + s];
+            const int tap = k / 3, ch = k - tap * 3;
+            const uint64_t plane = ch == 0 ? m : ch == 1 ? t : (~(m | t) & c4::kBoard);
+            const int off = (tap % 3 - 1) * 7 + (tap / 3 - 1);
+            v = off >= 0 ? plane >> off : plane << -off;
+        }
+        ((uint64_t *)(smem + kPlanes))[s * 32 + k] = v;
     }
-    if (wave == 0) head_layer<6>(smem, P, t0, lane);
-    else head_layer<5>(smem, P, t0, lane);
+    {
+        float *bias = (float *)(smem + kBias);
+        const int nres = 2 * P.blocks * kHid;
+        for (int i = tid; i < kHid + nres + 48; i += kThreads)
+            bias[i] = i < kHid ? P.b_stem[i] : i < kHid + nres ? P.b_res[i - kHid] : P.b_head[i - kHid - nres];
+    }
+    __syncthreads();
+    stamp(P, wave, lane, 0);
+    // head-linear weights -> LDS by LDS-DMA (38 x 1 KiB wave-instructions); in
+    // flight during the stem, retired by the barrier that follows it
+    for (int k = wave; k < kLinFloats / 256; k += kWaves)
+        __builtin_amdgcn_global_load_lds((const void *)(P.w_lin + k * 256 + lane * 4),
+                                         (__attribute__((address_space(3))) void *)(smem + kLin + k * 1024), 16, 0, 0);
+
+    switch (wave) {
+    case 0: torso_and_heads<0, FROM_X>(smem, P, x, base, valid, lane); break;
+    case 1: torso_and_heads<1, FROM_X>(smem, P, x, base, valid, lane); break;
+    case 2: torso_and_heads<2, FROM_X>(smem, P, x, base, valid, lane); break;
+    default: torso_and_heads<3, FROM_X>(smem, P, x, base, valid, lane); break;
+    }
     __syncthreads();
 
-    // linears: 64 (position, output) pairs x 4 partial sums; output 7 = value
+    stamp(P, wave, lane, 14);
+    // linears (connect_four.rs:63-64,69-70): 32 lanes per position, each lane a
+    // strided slice of the 1344 (policy) / 126 (value) inputs for all 8 outputs
+    // (weights from LDS), then a 32-lane reduction.
     {
         const float *H = (const float *)(smem + kH);
-        const int pair = tid >> 2, part = tid & 3;
-        const int s = pair >> 3, o = pair & 7;
-        float acc = 0.f;
-        if (o < c4::kActions) {
-            const float *h = H + s * kHeadC * c4::kCells;
-            const float *wr = P.w_pol + o * kPolIn;
-            for (int i = part * (kPolIn / 4); i < (part + 1) * (kPolIn / 4); ++i) acc += h[i] * wr[i];
-        } else {
-            const float *h = H + (s * kHeadC + 32) * c4::kCells;
-            for (int i = part; i < kValIn; i += 4) acc += h[i] * P.w_val[i];
+        const int s = tid >> 5, g = tid & 31;
+        const float *h = H + s * kHeadC * c4::kCells;
+        const float *wl = (const float *)(smem + kLin);
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int i4 = g; i4 < kPolIn / 4; i4 += 32) {
+            const float4 hv = *(const float4 *)(h + 4 * i4);
+#pragma unroll
+            for (int a = 0; a < c4::kActions; ++a) {
+                const float4 wv = *(const float4 *)(wl + a * kPolIn + 4 * i4);
+                acc[a] += hv.x * wv.x + hv.y * wv.y + hv.z * wv.z + hv.w * wv.w;
+            }
         }
-        acc += __shfl_xor(acc, 1, 4);
-        acc += __shfl_xor(acc, 2, 4);
-        if (part == 0) ((float *)(smem + kL))[s * 8 + o] = acc;
+        for (int i = g; i < kValIn; i += 32) acc[7] += h[kPolIn + i] * wl[c4::kActions * kPolIn + i];
+#pragma unroll
+        for (int m = 16; m >= 1; m >>= 1)
+#pragma unroll
+            for (int a = 0; a < 8; ++a) acc[a] += __shfl_xor(acc[a], m, 32);
+        if (g == 0) {
+            float *L = (float *)(smem + kL) + s * 8;
+#pragma unroll
+            for (int a = 0; a < 8; ++a) L[a] = acc[a];
+        }
     }
     __syncthreads();
+    stamp(P, wave, lane, 15);
     if (tid < valid) {
         const float *L = (const float *)(smem + kL) + tid * 8;
         const int slot = base + tid;
@@ -350,6 +470,7 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
             pr[1] = make_float4(out[4], out[5], out[6], 0.f);
         }
     }
+    stamp(P, wave, lane, 16);
 }
 
 // ---------------------------------------------------------------- host packing
@@ -392,7 +513,8 @@ size_t net_num_params(int game, int blocks, int hidden) {
 int net_create(spai_engine *e, int blocks, int hidden, const float *params, size_t nparams, spai_net **out) {
     SPAI_CHECK(e->game == SPAI_GAME_CONNECT4, SPAI_ERR_UNSUPPORTED, "device net: only Connect4 is built");
     SPAI_CHECK(hidden == kHid, SPAI_ERR_UNSUPPORTED, "device net: hidden must be 64 (got %d)", hidden);
-    SPAI_CHECK(blocks >= 0 && blocks <= 64, SPAI_ERR_INVALID, "bad block count %d", blocks);
+    SPAI_CHECK(blocks >= 0 && blocks <= kMaxBlocks, SPAI_ERR_UNSUPPORTED, "device net: 0..%d blocks (got %d)",
+               kMaxBlocks, blocks);
     SPAI_CHECK(params && nparams == net_num_params(e->game, blocks, hidden), SPAI_ERR_INVALID,
                "expected %zu params, got %zu", net_num_params(e->game, blocks, hidden), nparams);
     // walk the parameter list in construction order
@@ -484,9 +606,11 @@ int net_create(spai_engine *e, int blocks, int hidden, const float *params, size
     }
     up(n->w_head, wh);
     up(n->b_head, bh);
-    up(n->w_pol, std::vector<float>(pol_w, pol_w + 7 * kPolIn));
+    std::vector<float> wlin(kLinFloats, 0.f);
+    std::copy(pol_w, pol_w + 7 * kPolIn, wlin.begin());
+    std::copy(val_w, val_w + kValIn, wlin.begin() + 7 * kPolIn);
+    up(n->w_pol, wlin);
     up(n->b_pol, std::vector<float>(pol_b, pol_b + 7));
-    up(n->w_val, std::vector<float>(val_w, val_w + kValIn));
     up(n->b_val, std::vector<float>(val_b, val_b + 1));
     if (rc != SPAI_OK) {
         net_destroy(n);
@@ -516,12 +640,73 @@ static NetParams params_of(const spai_net *n) {
     P.b_stem = n->b_stem.p;
     P.b_res = n->b_res.p;
     P.b_head = n->b_head.p;
-    P.w_pol = n->w_pol.p;
+    P.w_lin = n->w_pol.p;
     P.b_pol = n->b_pol.p;
-    P.w_val = n->w_val.p;
     P.b_val = n->b_val.p;
+    P.stamps = nullptr;
     P.blocks = n->blocks;
     return P;
+}
+
+int ensure_io(spai_net *n, uint32_t cnt) {
+    if (n->io_value.n >= cnt) return SPAI_OK;
+    SPAI_TRY(n->io_x.alloc((size_t)cnt * 126));
+    SPAI_TRY(n->io_logits.alloc((size_t)cnt * 7));
+    SPAI_TRY(n->io_value.alloc(cnt));
+    SPAI_TRY(n->io_priors.alloc((size_t)cnt * kPriorStride));
+    SPAI_TRY(n->io_mine.alloc(cnt));
+    SPAI_TRY(n->io_theirs.alloc(cnt));
+    return SPAI_OK;
+}
+
+int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
+    SPAI_CHECK(cnt > 0, SPAI_ERR_INVALID, "need cnt > 0");
+    SPAI_TRY(ensure_io(n, cnt));
+    hipStream_t st = n->eng->stream;
+    std::vector<uint64_t> m(cnt), t(cnt);
+    uint64_t h = 0x1234;
+    for (uint32_t i = 0; i < cnt; ++i) {   // random reachable positions
+        c4::State s{0, 0, 0, c4::kOngoing};
+        h = c4::splitmix64(h);
+        for (int k = 0, plies = (int)(h % 30); k < plies; ++k) {
+            uint32_t lm = c4::legal_mask(s.x, s.o, s.status);
+            h = c4::splitmix64(h);
+            c4::State r;
+            c4::next_state(s, c4::kth_bit(lm, (int)(h % c4::popc32(lm))), r);
+            if (r.status != c4::kOngoing) break;
+            s = r;
+        }
+        const bool xm = c4::x_to_move(s.n);
+        m[i] = xm ? s.x : s.o;
+        t[i] = xm ? s.o : s.x;
+    }
+    const uint32_t grid = (cnt + kS - 1) / kS;
+    DevBuf<unsigned long long> d;
+    SPAI_TRY(d.alloc((size_t)grid * kWaves * kStamps));
+    SPAI_HIP(hipMemsetAsync(d.p, 0, d.n * 8, st));
+    SPAI_HIP(hipMemcpyAsync(n->io_mine.p, m.data(), (size_t)cnt * 8, hipMemcpyHostToDevice, st));
+    SPAI_HIP(hipMemcpyAsync(n->io_theirs.p, t.data(), (size_t)cnt * 8, hipMemcpyHostToDevice, st));
+    NetParams P = params_of(n);
+    P.stamps = d.p;
+    for (int rep = 0; rep < 3; ++rep)   // last launch warm
+        k_forward<false><<<grid, kThreads, 0, st>>>(nullptr, cnt, n->io_mine.p, n->io_theirs.p, nullptr, P,
+                                                   n->io_priors.p, n->io_value.p, nullptr);
+    SPAI_HIP(hipGetLastError());
+    std::vector<unsigned long long> hs(d.n);
+    SPAI_HIP(hipMemcpyAsync(hs.data(), d.p, d.n * 8, hipMemcpyDeviceToHost, st));
+    SPAI_HIP(hipStreamSynchronize(st));
+    // cycles[k] = mean over workgroups/waves of stamp[k] - stamp[0]; cycles[kStamps] = mean total
+    for (int k = 0; k < kStamps; ++k) cycles[k] = 0;
+    double cntw = 0;
+    for (uint32_t g = 0; g < grid; ++g)
+        for (int w = 0; w < kWaves; ++w) {
+            const unsigned long long *sp = hs.data() + ((size_t)g * kWaves + w) * kStamps;
+            if (!sp[0] || !sp[16]) continue;
+            for (int k = 0; k < kStamps; ++k) cycles[k] += sp[k] ? (double)(sp[k] - sp[0]) : 0.0;
+            cntw += 1;
+        }
+    for (int k = 0; k < kStamps; ++k) cycles[k] /= cntw > 0 ? cntw : 1;
+    return SPAI_OK;
 }
 
 int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint32_t max_n, const uint64_t *mine,
@@ -534,20 +719,10 @@ int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint3
     return SPAI_OK;
 }
 
-static int ensure(spai_net *n, uint32_t cnt) {
-    if (n->io_value.n >= cnt) return SPAI_OK;
-    SPAI_TRY(n->io_x.alloc((size_t)cnt * 126));
-    SPAI_TRY(n->io_logits.alloc((size_t)cnt * 7));
-    SPAI_TRY(n->io_value.alloc(cnt));
-    SPAI_TRY(n->io_priors.alloc((size_t)cnt * kPriorStride));
-    SPAI_TRY(n->io_mine.alloc(cnt));
-    SPAI_TRY(n->io_theirs.alloc(cnt));
-    return SPAI_OK;
-}
 
 int net_forward_x(spai_net *n, uint32_t cnt, const float *x, float *logits, float *value) {
     if (!cnt) return SPAI_OK;
-    SPAI_TRY(ensure(n, cnt));
+    SPAI_TRY(ensure_io(n, cnt));
     hipStream_t st = n->eng->stream;
     SPAI_HIP(hipMemcpyAsync(n->io_x.p, x, (size_t)cnt * 126 * 4, hipMemcpyHostToDevice, st));
     k_forward<true><<<(cnt + kS - 1) / kS, kThreads, 0, st>>>(nullptr, cnt, nullptr, nullptr, n->io_x.p, params_of(n),
@@ -561,7 +736,7 @@ int net_forward_x(spai_net *n, uint32_t cnt, const float *x, float *logits, floa
 
 int net_predict(spai_net *n, uint32_t cnt, const spai_c4_state *states, float *priors, float *values) {
     if (!cnt) return SPAI_OK;
-    SPAI_TRY(ensure(n, cnt));
+    SPAI_TRY(ensure_io(n, cnt));
     std::vector<uint64_t> m(cnt), t(cnt);
     for (uint32_t i = 0; i < cnt; ++i) {
         bool xm = c4::x_to_move(states[i].num_actions_played);

@@ -157,6 +157,7 @@ void net_destroy(spai_net *net);
 int net_forward_x(spai_net *net, uint32_t n, const float *x, float *logits, float *value);
 int net_predict(spai_net *net, uint32_t n, const spai_c4_state *states, float *priors, float *values);
 size_t net_num_params(int game, int blocks, int hidden);
+int net_phase_stamps(spai_net *net, uint32_t n, double *cycles);
 void net_init_params(int game, int blocks, int hidden, uint64_t seed, float *params);
 // evaluate `count` (device scalar) leaves of the batch; grid sized for max_n
 int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint32_t max_n,

@@ -32,6 +32,7 @@ SYMBOLS = [
     "spai_net_destroy", "spai_net_forward", "spai_predict", "spai_engine_set_net", "spai_trees_create",
     "spai_tree_reset", "spai_search", "spai_tree_use_subtree", "spai_tree_node", "spai_tree_size",
     "spai_selfplay_run", "spai_engine_set_timing", "spai_engine_timing", "spai_engine_timing_items",
+    "spai_net_phase_cycles",
 ]
 
 
@@ -107,6 +108,7 @@ def lib():
         L.spai_engine_set_timing.argtypes = [vp, i32]
         L.spai_engine_timing.argtypes = [vp, vp, vp]
         L.spai_engine_timing_items.argtypes = [vp, vp, vp]
+        L.spai_net_phase_cycles.argtypes = [vp, u32, vp]
         _lib = L
     return _lib
 
@@ -174,6 +176,11 @@ class Net:
         v = np.zeros(n, np.float32)
         _check(lib().spai_net_forward(self.h, n, _p(x), _p(lg), _p(v)))
         return lg, v
+
+    def phase_cycles(self, count=4096):
+        c = np.zeros(17, np.float64)
+        _check(lib().spai_net_phase_cycles(self.h, count, _p(c)))
+        return c
 
     def predict(self, states):
         a = states_array(states)
