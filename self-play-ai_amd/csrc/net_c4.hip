@@ -47,23 +47,23 @@ constexpr int kPolIn = 32 * c4::kCells;    // 1344
 constexpr int kValIn = 3 * c4::kCells;     // 126
 
 // LDS carve (bytes)
-constexpr int kZ = 0;                      // 128 B of zeros: row -1 of X
-constexpr int kX = 128;                    // [336][128 B] bf16 activations
-constexpr int kZ1 = kX + kP * 128;         // 128 B of zeros: row -1 of Y
-constexpr int kY = kZ1 + 128;              // second activation buffer
-constexpr int kH = kY;                     // fp32 head conv output [8][35][42] overlays Y
-constexpr int kHBytes = kS * kHeadC * c4::kCells * 4;
+constexpr int kZ = 0;                      // 256 B of zeros just below X (out-of-board taps)
+constexpr int kX = 256;                    // [336][128 B] bf16 activations (256-B aligned)
+constexpr int kZ1 = kX + kP * 128;         // 256 B of zeros just below Y
+constexpr int kY = kZ1 + 256;              // second activation buffer
+constexpr int kLinK = 1472;                // 35 x 42 = 1470 head features, padded to 46 k-steps of 32
+constexpr int kLinKSteps = kLinK / 32;     // 46
+constexpr int kH = kY;                     // bf16 head features [8][1472] overlay Y
+constexpr int kHBytes = kP * 128;          // (all of Y)
 constexpr int kB = kH + kHBytes;           // 8 x (mine, theirs)
-constexpr int kL = kB + kS * 16;           // logits scratch [8][8] f32
+constexpr int kL = kB + kS * 16;           // linear partials [4 waves][8][8] f32
 constexpr int kMaxBlocks = 20;
 constexpr int kBiasFloats = kHid + 2 * kMaxBlocks * kHid + 48;   // stem, residual convs, head
-constexpr int kBias = kL + kS * 8 * 4;     // all conv biases, staged once per workgroup
+constexpr int kBias = kL + kWaves * 64 * 4; // all conv biases, staged once per workgroup
 constexpr int kPlanes = kBias + kBiasFloats * 4;   // stem neighbour planes [8][32] u64
-constexpr int kLinFloats = 9728;           // policy [7][1344] + value [126] + pad to 38 KiB
-constexpr int kLin = kPlanes + kS * 32 * 8;        // head linear weights (LDS-DMA at kernel start)
-constexpr int kLdsBytes = kLin + kLinFloats * 4;
+constexpr int kLdsBytes = kPlanes + kS * 32 * 8;
 constexpr int kStamps = 17;                // phase stamps per wave in the diagnostic mode
-static_assert(kY + kP * 128 <= kB, "heads overlay");
+static_assert(kS * kLinK * 2 <= kHBytes, "head features fit in Y");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 
 struct NetParams {
@@ -73,7 +73,7 @@ struct NetParams {
     const float *b_stem;   // [64]
     const float *b_res;    // [2*blocks][64]
     const float *b_head;   // [48]
-    const float *w_lin;    // [7][1344] policy | [126] value | zero pad, kLinFloats
+    const uint4 *w_lin;    // [46 ks][64] B fragments of the fused policy|value linear
     const float *b_pol;    // [7]
     const float *b_val;    // [1]
     unsigned long long *stamps;   // diagnostic: [grid][4 waves][kStamps] s_memtime, or null
@@ -108,8 +108,9 @@ struct Plan {
 // Per-lane LDS geometry, computed once per kernel (positions are the same for
 // every layer).  For tile t and tap (dh,dw) the B-fragment address relative to
 // the activation buffer is rel[t][tap] (k-step half 0; half 1 = rel ^ 64, the
-// swizzled chunk index flips bit 2).  An out-of-board tap points at row -1 of
-// the buffer, a zeroed 128-B row, so the k-loop needs no select.  epi[t] is the
+// swizzled chunk index flips bit 2).  With the XOR swizzle every 3x3 shift of a
+// 16-row tile is conflict-free for ds_read_b128; an out-of-board tap points
+// into the zeroed 256-B block below the buffer, so the k-loop needs no select.  epi[t] is the
 // relative address of this lane's 4 output channels of co tile 0 at its
 // position (co tile c: epi ^ (c << 5)).
 template <int NT>
@@ -132,7 +133,10 @@ __device__ __forceinline__ void make_geo(int lane, Geo<Plan<W, CT>::NT> &g) {
             const int dh = tap / 3 - 1, dw = tap % 3 - 1;
             const int r = p + dh * c4::kCols + dw;
             const bool ok = (unsigned)(h + dh) < (unsigned)c4::kRows && (unsigned)(w + dw) < (unsigned)c4::kCols;
-            g.rel[t][tap] = ok ? r * 128 + ((q ^ (r & 7)) << 4) : -128 + (q << 4);
+            const int full = r * 128 + ((q ^ (r & 7)) << 4);
+            // an out-of-board tap reads the zero block below the buffer at the same
+            // 16-B granule its row would use, so it never adds a bank conflict
+            g.rel[t][tap] = ok ? full : (full & 255) - 256;
         }
         g.epi[t] = p * 128 + ((((q >> 1)) ^ (p & 7)) << 4) + ((q & 1) << 3);
     }
@@ -305,7 +309,7 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
     conv_mfma<W, kHeadCT, kX>(smem, g, (const float *)(smem + kBias) + kHid * (1 + 2 * P.blocks), P.w_head, nullptr,
                               lane, A, acc);
     const int col = lane & 15, q = lane >> 4;
-    float *H = (float *)(smem + kH);
+    uint16_t *H = (uint16_t *)(smem + kH);
 #pragma unroll
     for (int i = 0; i < PL::n; ++i) {
         const int co0 = PL::co(i) * 16 + 4 * q;
@@ -314,8 +318,34 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int co = co0 + r;
-            if (co < kHeadC) H[(s * kHeadC + co) * c4::kCells + cell] = fmaxf(acc[i][r], 0.f);
+            if (co < kHeadC)
+                H[s * kLinK + co * c4::kCells + cell] = __builtin_bit_cast(uint16_t, (__bf16)fmaxf(acc[i][r], 0.f));
         }
+    }
+    if (W == 0 && lane < kS * 2) H[(lane >> 1) * kLinK + kHeadC * c4::kCells + (lane & 1)] = 0;   // K padding
+}
+
+// fused policy|value linear on MFMA: out[s][o] = sum_k H[s][k] * Wl[o][k]
+// (o < 7 policy logits over k < 1344, o = 7 value pre-activation over
+// 1344 <= k < 1470; connect_four.rs:63-64,69-70).  Wave W takes k-steps
+// [12W, 12W+12) of 46; partial sums go to LDS.
+template <int W>
+__device__ __forceinline__ void linear_mfma(uint8_t *smem, const NetParams &P, int lane) {
+    constexpr int k0 = 12 * W, k1 = (12 * (W + 1) < kLinKSteps) ? 12 * (W + 1) : kLinKSteps;
+    const int s = lane & 15, q = lane >> 4;
+    const uint8_t *hrow = s < kS ? smem + kH + s * kLinK * 2 + q * 16 : smem + kZ + q * 16;
+    const int hstep = s < kS ? 64 : 0;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = k0; ks < k1; ++ks) {
+        const uint4 a = *(const uint4 *)(hrow + ks * hstep);
+        const uint4 b = P.w_lin[ks * 64 + lane];
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(b), acc, 0, 0, 0);
+    }
+    float *L = (float *)(smem + kL) + W * 64;   // D[row s = 4q + r][col o = lane & 15]
+    if (q < 2 && (lane & 15) < 8) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) L[(4 * q + r) * 8 + (lane & 15)] = acc[r];
     }
 }
 
@@ -345,6 +375,9 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
         if (l2 < 12) stamp(P, W, lane, 2 + l2);
     }
     head_layer<W>(smem, P, lane);
+    __syncthreads();
+    stamp(P, W, lane, 14);
+    linear_mfma<W>(smem, P, lane);
 }
 
 template <bool FROM_X>
@@ -360,8 +393,8 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
-    if (tid < 32) ((uint32_t *)(smem + kZ))[tid] = 0u;
-    else if (tid < 64) ((uint32_t *)(smem + kZ1))[tid - 32] = 0u;
+    if (tid < 64) ((uint32_t *)(smem + kZ))[tid] = 0u;
+    else if (tid < 128) ((uint32_t *)(smem + kZ1))[tid - 64] = 0u;
     if (tid < kS) {
         uint64_t m = 0, t = 0;
         if (!FROM_X && tid < valid) {
@@ -391,11 +424,6 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
     }
     __syncthreads();
     stamp(P, wave, lane, 0);
-    // head-linear weights -> LDS by LDS-DMA (38 x 1 KiB wave-instructions); in
-    // flight during the stem, retired by the barrier that follows it
-    for (int k = wave; k < kLinFloats / 256; k += kWaves)
-        __builtin_amdgcn_global_load_lds((const void *)(P.w_lin + k * 256 + lane * 4),
-                                         (__attribute__((address_space(3))) void *)(smem + kLin + k * 1024), 16, 0, 0);
 
     switch (wave) {
     case 0: torso_and_heads<0, FROM_X>(smem, P, x, base, valid, lane); break;
@@ -404,49 +432,22 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
     default: torso_and_heads<3, FROM_X>(smem, P, x, base, valid, lane); break;
     }
     __syncthreads();
-
-    stamp(P, wave, lane, 14);
-    // linears (connect_four.rs:63-64,69-70): 32 lanes per position, each lane a
-    // strided slice of the 1344 (policy) / 126 (value) inputs for all 8 outputs
-    // (weights from LDS), then a 32-lane reduction.
-    {
-        const float *H = (const float *)(smem + kH);
-        const int s = tid >> 5, g = tid & 31;
-        const float *h = H + s * kHeadC * c4::kCells;
-        const float *wl = (const float *)(smem + kLin);
-        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int i4 = g; i4 < kPolIn / 4; i4 += 32) {
-            const float4 hv = *(const float4 *)(h + 4 * i4);
-#pragma unroll
-            for (int a = 0; a < c4::kActions; ++a) {
-                const float4 wv = *(const float4 *)(wl + a * kPolIn + 4 * i4);
-                acc[a] += hv.x * wv.x + hv.y * wv.y + hv.z * wv.z + hv.w * wv.w;
-            }
-        }
-        for (int i = g; i < kValIn; i += 32) acc[7] += h[kPolIn + i] * wl[c4::kActions * kPolIn + i];
-#pragma unroll
-        for (int m = 16; m >= 1; m >>= 1)
-#pragma unroll
-            for (int a = 0; a < 8; ++a) acc[a] += __shfl_xor(acc[a], m, 32);
-        if (g == 0) {
-            float *L = (float *)(smem + kL) + s * 8;
-#pragma unroll
-            for (int a = 0; a < 8; ++a) L[a] = acc[a];
-        }
-    }
-    __syncthreads();
     stamp(P, wave, lane, 15);
     if (tid < valid) {
-        const float *L = (const float *)(smem + kL) + tid * 8;
+        const float *L = (const float *)(smem + kL);
         const int slot = base + tid;
+        float sum8[8];
+#pragma unroll
+        for (int o = 0; o < 8; ++o)
+            sum8[o] = L[tid * 8 + o] + L[64 + tid * 8 + o] + L[128 + tid * 8 + o] + L[192 + tid * 8 + o];
         float lg[c4::kActions];
         float mx = -INFINITY;
 #pragma unroll
         for (int a = 0; a < c4::kActions; ++a) {
-            lg[a] = L[a] + P.b_pol[a];
+            lg[a] = sum8[a] + P.b_pol[a];
             mx = fmaxf(mx, lg[a]);
         }
-        const float v = tanhf(L[7] + P.b_val[0]);
+        const float v = tanhf(sum8[7] + P.b_val[0]);
         value[slot] = v;
         if (logits) {
 #pragma unroll
@@ -606,10 +607,19 @@ int net_create(spai_engine *e, int blocks, int hidden, const float *params, size
     }
     up(n->w_head, wh);
     up(n->b_head, bh);
-    std::vector<float> wlin(kLinFloats, 0.f);
-    std::copy(pol_w, pol_w + 7 * kPolIn, wlin.begin());
-    std::copy(val_w, val_w + kValIn, wlin.begin() + 7 * kPolIn);
-    up(n->w_pol, wlin);
+    // fused linear as MFMA B fragments: [ks 46][lane 64][8], lane -> o = lane & 15,
+    // k = ks*32 + 8*(lane>>4) + j over the head features H[s][c*42 + cell]
+    std::vector<uint16_t> wlin((size_t)kLinKSteps * 64 * 8, 0);
+    for (int ks = 0; ks < kLinKSteps; ++ks)
+        for (int l = 0; l < 64; ++l)
+            for (int j = 0; j < 8; ++j) {
+                const int o = l & 15, k = ks * 32 + 8 * (l >> 4) + j;
+                float v = 0.f;
+                if (o < 7 && k < kPolIn) v = pol_w[(size_t)o * kPolIn + k];
+                else if (o == 7 && k >= kPolIn && k < kPolIn + kValIn) v = val_w[k - kPolIn];
+                wlin[((size_t)ks * 64 + l) * 8 + j] = f2bf(v);
+            }
+    up(n->w_lin, wlin);
     up(n->b_pol, std::vector<float>(pol_b, pol_b + 7));
     up(n->b_val, std::vector<float>(val_b, val_b + 1));
     if (rc != SPAI_OK) {
@@ -622,8 +632,8 @@ int net_create(spai_engine *e, int blocks, int hidden, const float *params, size
 
 void net_destroy(spai_net *n) {
     if (!n) return;
-    for (auto *b : {&n->w_stem, &n->w_res, &n->w_head}) b->release();
-    for (auto *b : {&n->b_stem, &n->b_res, &n->b_head, &n->w_pol, &n->b_pol, &n->w_val, &n->b_val, &n->io_x,
+    for (auto *b : {&n->w_stem, &n->w_res, &n->w_head, &n->w_lin}) b->release();
+    for (auto *b : {&n->b_stem, &n->b_res, &n->b_head, &n->b_pol, &n->b_val, &n->io_x,
                     &n->io_logits, &n->io_value, &n->io_priors})
         b->release();
     n->io_mine.release();
@@ -640,7 +650,7 @@ static NetParams params_of(const spai_net *n) {
     P.b_stem = n->b_stem.p;
     P.b_res = n->b_res.p;
     P.b_head = n->b_head.p;
-    P.w_lin = n->w_pol.p;
+    P.w_lin = (const uint4 *)n->w_lin.p;
     P.b_pol = n->b_pol.p;
     P.b_val = n->b_val.p;
     P.stamps = nullptr;

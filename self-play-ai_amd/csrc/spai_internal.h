@@ -116,8 +116,8 @@ struct spai_net {
     spai_engine *eng = nullptr;
     int blocks = 0, hidden = 0;
     // packed, BN-folded bf16 MFMA fragments + fp32 biases / head linears (see net_c4.hip)
-    spai::DevBuf<uint16_t> w_stem, w_res, w_head;
-    spai::DevBuf<float> b_stem, b_res, b_head, w_pol, b_pol, w_val, b_val;
+    spai::DevBuf<uint16_t> w_stem, w_res, w_head, w_lin;
+    spai::DevBuf<float> b_stem, b_res, b_head, b_pol, b_val;
     spai::DevBuf<float> io_x, io_logits, io_value, io_priors;   // scratch for forward/predict calls
     spai::DevBuf<uint64_t> io_mine, io_theirs;
     spai::DevBuf<uint32_t> io_count;
