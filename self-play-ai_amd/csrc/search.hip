@@ -15,6 +15,8 @@
 // per search call, the sampled child goes down as the new root.
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "philox.h"
@@ -516,10 +518,17 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
     std::vector<float> enc, sp, sv;
     double sims = 0, evals = 0, games = 0, positions = 0, moves = 0;
     uint64_t move_no = 0;
+    // optional per-move trace (diagnostics): SPAI_TRACE_MOVES=<csv path>
+    FILE *trace = nullptr;
+    if (const char *tp = std::getenv("SPAI_TRACE_MOVES")) trace = std::fopen(tp, "a");
     while (!active.empty()) {
         const uint32_t na = (uint32_t)active.size();
         double ev = 0;
+        const auto tm0 = std::chrono::steady_clock::now();
         SPAI_TRY(search(e, na, active.data(), e->cfg.num_searches, pol.data(), ids.data(), vis.data(), nch.data(), &ev));
+        if (trace)
+            std::fprintf(trace, "%llu,%u,%.0f,%.6f\n", (unsigned long long)move_no, na, ev,
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - tm0).count());
         sims += (double)na * e->cfg.num_searches;
         evals += ev;
         moves += 1;
@@ -572,6 +581,7 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
         SPAI_TRY(upload_roots(e, 0, T.n_trees));
         ++move_no;
     }
+    if (trace) std::fclose(trace);
     if (stats) {
         stats->sims = sims;
         stats->evals = evals;
