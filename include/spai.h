@@ -181,9 +181,11 @@ int spai_engine_timing(spai_engine *eng, double *avg_ms, double *launches);
  * launches covered (trees for select/expand, evaluated leaves for the forward) */
 int spai_engine_timing_items(spai_engine *eng, double *total_ms, double *items);
 /* Diagnostic build-in: one forward over `count` random positions with s_memtime
- * stamps at every phase boundary of the fused kernel.  cycles[k] = mean shader
- * cycles from kernel start to stamp k (0 start, 1 stem, 2..13 residual convs,
- * 14 head conv, 15 linears, 16 end).  Never used on the timed path. */
+ * stamps at every phase boundary of the fused kernel.  cycles[k] (k < 20) = mean
+ * shader cycles from group start to stamp k (0 start, 1 stem, 2..13 residual
+ * convs, 14 head conv, 15 linears, 16 end; 17/18/19 = block 0 conv1 k-loop end,
+ * epilogue end, barrier passed).  Needs the diagnostic build (SPAI_DIAG);
+ * the production library returns SPAI_ERR_UNSUPPORTED.  Never on the timed path. */
 int spai_net_phase_cycles(spai_net *net, uint32_t count, double *cycles);
 
 #ifdef __cplusplus

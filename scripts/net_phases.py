@@ -15,5 +15,12 @@ for n in (2048, 4096):
     d = np.diff(c)
     print(f"batch {n}: total {c[16]:.0f} cycles/wave = {c[16] / 2.1e3:.1f} us @2.1GHz")
     print("  " + "  ".join(f"{names[k + 1]}={d[k]:.0f}" for k in range(16)))
+# per-group latency for every group size S (one group per workgroup, 256 workgroups)
+for S in range(1, 9):
+    os.environ["SPAI_PHASE_S"] = str(S)
+    c = net.phase_cycles(256 * S)
+    print(f"S={S}: {c[16]:.0f} cycles/wave = {c[16] / 2.1e3:.1f} us @2.1GHz  (res layer ~{np.diff(c)[3]:.0f}; "
+          f"block0 conv1: k-loop {c[17] - c[1]:.0f}, epilogue {c[18] - c[17]:.0f}, barrier {c[19] - c[18]:.0f})")
+os.environ.pop("SPAI_PHASE_S")
 net.close()
 e.close()

@@ -25,6 +25,7 @@
 // Algorithmic FLOPs per position (6 blocks x 64): 39,016,572.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "spai_internal.h"
@@ -34,10 +35,15 @@ namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kHid = 64;
-constexpr int kS = 8;                      // positions per workgroup
-constexpr int kP = kS * c4::kCells;        // 336 board cells per workgroup
+constexpr int kS = 8;                      // max positions per workgroup group
+constexpr int kP = kS * c4::kCells;        // 336 board cells (LDS rows) at S = 8
+// position tiles (16 LDS rows each) for a group of S positions
+__host__ __device__ constexpr int npt_of(int S) { return (S * c4::kCells + 15) / 16; }
 constexpr int kWaves = 4;
 constexpr int kThreads = kWaves * 64;
 constexpr int kKStepsRes = 18;             // 576 / 32
@@ -62,7 +68,7 @@ constexpr int kBiasFloats = kHid + 2 * kMaxBlocks * kHid + 48;   // stem, residu
 constexpr int kBias = kL + kWaves * 64 * 4; // all conv biases, staged once per workgroup
 constexpr int kPlanes = kBias + kBiasFloats * 4;   // stem neighbour planes [8][32] u64
 constexpr int kLdsBytes = kPlanes + kS * 32 * 8;
-constexpr int kStamps = 17;                // phase stamps per wave in the diagnostic mode
+constexpr int kStamps = 20;                // phase stamps per wave in the diagnostic mode (17..19: inside block 0 conv1)
 static_assert(kS * kLinK * 2 <= kHBytes, "head features fit in Y");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 
@@ -80,29 +86,78 @@ struct NetParams {
     int blocks;
 };
 
+// Phase stamps exist only in the diagnostic build (-DSPAI_DIAG): the branch
+// around the store would otherwise cost the production kernel precise
+// vmcnt tracking (hipcc waits vmcnt(0) after such control flow).
 __device__ __forceinline__ void stamp(const NetParams &P, int wave, int lane, int k) {
+#ifdef SPAI_DIAG
     if (P.stamps && lane == 0) P.stamps[((size_t)blockIdx.x * kWaves + wave) * kStamps + k] = __builtin_amdgcn_s_memtime();
+#endif
 }
 
 __device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
 
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-    __bf16 ha = (__bf16)a, hb = (__bf16)b;
-    return (uint32_t)__builtin_bit_cast(uint16_t, ha) | ((uint32_t)__builtin_bit_cast(uint16_t, hb) << 16);
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
 }
 
-// Work split: a conv layer is 21 position tiles x CT co tiles = 21*CT tile-tasks
-// (task = pos_tile*CT + co_tile).  Wave W owns tasks [TT*W/4, TT*(W+1)/4): 21
-// each for the 64-channel layers, so all four SIMDs issue the same MFMA count.
-template <int W, int CT>
+// relu(round_bf16(a)), relu(round_bf16(b)) packed: ReLU on the packed bf16 pair is a
+// signed 16-bit max with 0 (a negative value rounds to a negative bf16 or -0,
+// both of which clamp to +0), so it costs one v_pk_max_i16 per two channels.
+__device__ __forceinline__ uint32_t pack_relu_bf16x2(float a, float b) {
+    const i16x2 h = __builtin_bit_cast(i16x2, __builtin_convertvector((f32x2){a, b}, bf16x2));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(h, (i16x2){0, 0}));
+}
+
+// Work split: a conv layer is NPT position tiles x CT co tiles = NPT*CT
+// tile-tasks over the four waves.  Three task orders, picked per layer shape:
+//  * position-major (head conv, CT = 3, and the largest groups, where the
+//    other orders run out of registers): wave W owns tasks [TT*W/4, TT*(W+1)/4)
+//    of task = pos_tile*CT + co_tile: ~NPT/4 position tiles, every co tile, so
+//    each wave streams all CT weight fragments per k-step;
+//  * co-major (64-channel layers, NPT <= SPAI_CO_MAJOR_MAX_NPT): wave W owns co
+//    tile W over all NPT position tiles, so the CU fetches each weight fragment
+//    once per k-step (4 KiB) at NPT LDS reads per wave;
+//  * pair split (64-channel layers, NPT <= SPAI_PAIR_MAX_NPT): wave (j = W>>1, h = W&1) owns co
+//    tiles {2j, 2j+1} over position tiles [h*m, h*m+m) (m = NPT/2) plus, for
+//    odd NPT, the last tile in co tile 2j+h: NPT tasks per wave, 2 weight
+//    fragments per wave and k-step (8 KiB per CU), ~NPT/2 LDS reads.
+// The per-CU weight stream is what bounds small groups: the vector-memory
+// path delivers ~64 B/clk/CU, i.e. 16 KiB per k-step costs ~256 cycles.
+// Position tiles are addressed through a local index t < NT; gpt(t) is the
+// group's position tile, pt(i) the local tile and co(i) the co tile of task i.
+#ifndef SPAI_CO_MAJOR_MAX_NPT
+#define SPAI_CO_MAJOR_MAX_NPT 8
+#endif
+#ifndef SPAI_PAIR_MAX_NPT
+#define SPAI_PAIR_MAX_NPT 11
+#endif
+template <int W, int CT, int NPT>
 struct Plan {
-    static constexpr int TT = 21 * CT;
+    static constexpr int MODE = CT != 4 ? 0 : NPT <= SPAI_CO_MAJOR_MAX_NPT ? 1 : NPT <= SPAI_PAIR_MAX_NPT ? 2 : 0;
+    static constexpr int TT = NPT * CT;
+    // position-major / co-major: a contiguous task range
     static constexpr int first = TT * W / 4;
-    static constexpr int n = TT * (W + 1) / 4 - first;      // tasks of this wave
-    static constexpr int T0 = first / CT;                   // first position tile touched
-    static constexpr int NT = (first + n - 1) / CT - T0 + 1;  // position tiles touched (<= 6)
-    static constexpr int pt(int i) { return (first + i) / CT - T0; }
-    static constexpr int co(int i) { return (first + i) % CT; }
+    static constexpr int nr = TT * (W + 1) / 4 - first;
+    static constexpr int last = first + nr - 1;
+    // pair split
+    static constexpr int m = NPT / 2, r = NPT % 2, pj = W >> 1, ph = W & 1;
+
+    static constexpr int n = MODE == 2 ? 2 * m + r : nr;   // tasks of this wave
+    static constexpr int C0 = MODE == 2 ? 2 * pj : MODE == 1 ? first / NPT : 0;   // first co tile loaded
+    static constexpr int CTL = MODE == 2 ? 2 : MODE == 1 ? last / NPT - C0 + 1 : CT;   // co tiles per k-step
+    static constexpr int T0 = MODE == 2 ? ph * m
+                              : MODE == 1 ? (CTL == 1 ? first % NPT : 0)
+                                          : first / CT;
+    static constexpr int NT = MODE == 2 ? m + r : MODE == 1 ? (CTL == 1 ? nr : NPT) : last / CT - T0 + 1;
+    static constexpr int gpt(int t) { return MODE == 2 && t == m ? NPT - 1 : T0 + t; }
+    static constexpr int pt(int i) {
+        return MODE == 2 ? (i < 2 * m ? i / 2 : m) : (MODE == 1 ? (first + i) % NPT : (first + i) / CT) - T0;
+    }
+    static constexpr int co(int i) {
+        return MODE == 2 ? (i < 2 * m ? 2 * pj + (i & 1) : 2 * pj + ph)
+                         : MODE == 1 ? (first + i) / NPT : (first + i) % CT;
+    }
 };
 
 // Per-lane LDS geometry, computed once per kernel (positions are the same for
@@ -119,13 +174,13 @@ struct Geo {
     int epi[NT];
 };
 
-template <int W, int CT>
-__device__ __forceinline__ void make_geo(int lane, Geo<Plan<W, CT>::NT> &g) {
-    using PL = Plan<W, CT>;
+template <int W, int CT, int NPT>
+__device__ __forceinline__ void make_geo(int lane, Geo<Plan<W, CT, NPT>::NT> &g) {
+    using PL = Plan<W, CT, NPT>;
     const int col = lane & 15, q = lane >> 4;
 #pragma unroll
     for (int t = 0; t < PL::NT; ++t) {
-        const int p = (PL::T0 + t) * 16 + col;
+        const int p = PL::gpt(t) * 16 + col;
         const int cell = p % c4::kCells;
         const int h = cell / c4::kCols, w = cell - h * c4::kCols;
 #pragma unroll
@@ -142,94 +197,119 @@ __device__ __forceinline__ void make_geo(int lane, Geo<Plan<W, CT>::NT> &g) {
     }
 }
 
+// Prefetch depths per group size: a small group has few MFMAs per k-step to
+// hide a weight load (L2) or an LDS read behind, but registers to spare.
+// (DA must divide the 18 k-steps of a layer: the ring carries the next layer's
+// first DA-1 k-steps in the slots a fresh layer expects.)
+__host__ __device__ constexpr int a_depth(int S) { return S <= 2 ? 9 : S <= 4 ? 6 : 3; }
+__host__ __device__ constexpr int b_depth(int S) { return S <= 2 ? 4 : S <= 3 ? 3 : 2; }
+
 // implicit-GEMM 3x3 conv over the LDS activations at IN for wave W's tasks.
-// Software pipeline: A (weights, global/L2) two k-steps ahead, B (LDS) one
-// k-step ahead; sched_group_barrier interleaves the prefetch with the MFMAs
+// Software pipeline: A (weights, global/L2) DA-1 k-steps ahead, B (LDS) DB-1
+// k-steps ahead; sched_group_barrier interleaves the prefetch with the MFMAs
 // (and keeps the scheduler from sinking loads onto their uses).  The first
 // k-step takes the bias as its C operand, so the accumulators need no zeroing
-// and the epilogue no bias add.  The A ring is the caller's: A[0], A[1] arrive
-// holding k-steps 0 and 1, and the last two k-steps refill them with k-steps 0
-// and 1 of the next layer (`wn`, may be null), so consecutive layers stream
-// weights without a cold start.
-template <int W, int CT, int IN>
-__device__ __forceinline__ void conv_mfma(const uint8_t *smem, const Geo<Plan<W, CT>::NT> &g, const float *bias,
+// and the epilogue no bias add.  The A ring is the caller's: A[0..DA-2] arrive
+// holding k-steps 0..DA-2, and the last DA-1 k-steps refill them with the first
+// k-steps of the next layer (`wn`, may be null), so consecutive layers stream
+// weights without a cold start.  `wn` is always a valid layer (the current one
+// when nothing follows): an unconditional prefetch keeps the vmcnt bookkeeping
+// free of branches.
+template <int W, int CT, int NPT, int IN, int DA, int DB>
+__device__ __forceinline__ void conv_mfma(const uint8_t *smem, const Geo<Plan<W, CT, NPT>::NT> &g, const float *bias,
                                           const uint4 *__restrict__ w, const uint4 *__restrict__ wn, int lane,
-                                          uint4 (&A)[3][CT], f32x4 (&acc)[Plan<W, CT>::n]) {
-    using PL = Plan<W, CT>;
-    constexpr int NT = PL::NT;
+                                          uint4 (&A)[DA][Plan<W, CT, NPT>::CTL],
+                                          f32x4 (&acc)[Plan<W, CT, NPT>::n]) {
+    using PL = Plan<W, CT, NPT>;
+    constexpr int NT = PL::NT, CTL = PL::CTL;
+    static_assert(kKStepsRes % DA == 0, "the carried A ring needs DA | k-steps per layer");
     const int q = lane >> 4;
-    f32x4 bv[CT];
+    f32x4 bv[CTL];
 #pragma unroll
-    for (int c = 0; c < CT; ++c) {
-        const float4 b = *(const float4 *)(bias + c * 16 + 4 * q);
+    for (int c = 0; c < CTL; ++c) {
+        const float4 b = *(const float4 *)(bias + (PL::C0 + c) * 16 + 4 * q);
         bv[c] = f32x4{b.x, b.y, b.z, b.w};
     }
-    const uint4 *wl = w + lane;
-    const uint4 *wnl = wn ? wn + lane : nullptr;
-    uint4 B[2][NT];
+    const uint4 *wl = w + PL::C0 * 64 + lane;
+    const uint4 *wnl = wn + PL::C0 * 64 + lane;
+    uint4 B[DB][NT];
 #pragma unroll
-    for (int t = 0; t < NT; ++t) B[0][t] = *(const uint4 *)(smem + IN + g.rel[t][0]);
+    for (int kb = 0; kb < DB - 1; ++kb) {
+        const int tap = kb >> 1, flip = (kb & 1) << 6;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) B[kb][t] = *(const uint4 *)(smem + IN + (g.rel[t][tap] ^ flip));
+    }
 #pragma unroll
     for (int ks = 0; ks < kKStepsRes; ++ks) {
-        if (ks + 2 < kKStepsRes) {
+        constexpr int la = DA - 1, lb = DB - 1;
+        if (ks + la < kKStepsRes) {
 #pragma unroll
-            for (int c = 0; c < CT; ++c) A[(ks + 2) % 3][c] = wl[((ks + 2) * CT + c) * 64];
-        } else if (wnl) {
+            for (int c = 0; c < CTL; ++c)
+#ifdef SPAI_EXP_A_FIXED
+                A[(ks + la) % DA][c] = wl[c * 64];
+#else
+                A[(ks + la) % DA][c] = wl[((ks + la) * CT + c) * 64];
+#endif
+        } else {
 #pragma unroll
-            for (int c = 0; c < CT; ++c) A[(ks + 2) % 3][c] = wnl[((ks + 2 - kKStepsRes) * CT + c) * 64];
+            for (int c = 0; c < CTL; ++c) A[(ks + la) % DA][c] = wnl[((ks + la - kKStepsRes) * CT + c) * 64];
         }
-        if (ks + 1 < kKStepsRes) {
-            const int tap = (ks + 1) >> 1, flip = ((ks + 1) & 1) << 6;
+        if (ks + lb < kKStepsRes) {
+            const int tap = (ks + lb) >> 1, flip = ((ks + lb) & 1) << 6;
 #pragma unroll
-            for (int t = 0; t < NT; ++t) B[(ks + 1) % 2][t] = *(const uint4 *)(smem + IN + (g.rel[t][tap] ^ flip));
+            for (int t = 0; t < NT; ++t) B[(ks + lb) % DB][t] = *(const uint4 *)(smem + IN + (g.rel[t][tap] ^ flip));
         }
 #pragma unroll
         for (int i = 0; i < PL::n; ++i)
-            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[ks % 3][PL::co(i)]),
-                                                            as_bf16x8(B[ks % 2][PL::pt(i)]),
-                                                            ks == 0 ? bv[PL::co(i)] : acc[i], 0, 0, 0);
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[ks % DA][PL::co(i) - PL::C0]),
+                                                            as_bf16x8(B[ks % DB][PL::pt(i)]),
+                                                            ks == 0 ? bv[PL::co(i) - PL::C0] : acc[i], 0, 0, 0);
         // issue order for this k-step: each MFMA followed by up to 2 VALU, one
-        // LDS read (next B) and one weight load (A, two ahead)
+        // LDS read (next B) and one weight load (A, DA-1 ahead)
 #pragma unroll
         for (int i = 0; i < PL::n; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
             if (i < NT) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            if (i < CT) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            if (i < CTL) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
     }
 }
 
-template <int CT>
-__device__ __forceinline__ void load_a01(const uint4 *__restrict__ w, int lane, uint4 (&A)[3][CT]) {
+template <int CT, int C0, int CTL, int DA>
+__device__ __forceinline__ void load_a_first(const uint4 *__restrict__ w, int lane, uint4 (&A)[DA][CTL]) {
 #pragma unroll
-    for (int c = 0; c < CT; ++c) {
-        A[0][c] = w[c * 64 + lane];
-        A[1][c] = w[(CT + c) * 64 + lane];
-    }
+    for (int k = 0; k < DA - 1; ++k)
+#pragma unroll
+        for (int c = 0; c < CTL; ++c) A[k][c] = w[(k * CT + C0 + c) * 64 + lane];
 }
 
-// epilogue for a 64-channel bf16 output: relu(acc [+ residual]) -> LDS at OUT
-template <int W, int OUT, bool RESIDUAL>
-__device__ __forceinline__ void epilogue_act(uint8_t *smem, const Geo<Plan<W, 4>::NT> &g, f32x4 (&acc)[Plan<W, 4>::n]) {
-    using PL = Plan<W, 4>;
+// epilogue for a 64-channel bf16 output: relu(acc [+ residual]) -> LDS at OUT.
+// The residual reads are all issued before the first use so their LDS latency
+// is paid once, not once per tile.
+template <int W, int NPT, int OUT, bool RESIDUAL>
+__device__ __forceinline__ void epilogue_act(uint8_t *smem, const Geo<Plan<W, 4, NPT>::NT> &g, f32x4 (&acc)[Plan<W, 4, NPT>::n]) {
+    using PL = Plan<W, 4, NPT>;
+#ifdef SPAI_EXP_NO_EPI
+    if (acc[0][0] != 12345.f) return;
+#endif
+    uint2 r[RESIDUAL ? PL::n : 1];
+    if (RESIDUAL) {
+#pragma unroll
+        for (int i = 0; i < PL::n; ++i) r[i] = *(const uint2 *)(smem + OUT + (g.epi[PL::pt(i)] ^ (PL::co(i) << 5)));
+    }
 #pragma unroll
     for (int i = 0; i < PL::n; ++i) {
         const int off = OUT + (g.epi[PL::pt(i)] ^ (PL::co(i) << 5));
         float v0 = acc[i][0], v1 = acc[i][1], v2 = acc[i][2], v3 = acc[i][3];
         if (RESIDUAL) {
-            const uint2 r = *(const uint2 *)(smem + off);
-            v0 += __builtin_bit_cast(float, r.x << 16);
-            v1 += __builtin_bit_cast(float, r.x & 0xFFFF0000u);
-            v2 += __builtin_bit_cast(float, r.y << 16);
-            v3 += __builtin_bit_cast(float, r.y & 0xFFFF0000u);
+            v0 += __builtin_bit_cast(float, r[i].x << 16);
+            v1 += __builtin_bit_cast(float, r[i].x & 0xFFFF0000u);
+            v2 += __builtin_bit_cast(float, r[i].y << 16);
+            v3 += __builtin_bit_cast(float, r[i].y & 0xFFFF0000u);
         }
-        v0 = fmaxf(v0, 0.f);
-        v1 = fmaxf(v1, 0.f);
-        v2 = fmaxf(v2, 0.f);
-        v3 = fmaxf(v3, 0.f);
-        *(uint2 *)(smem + off) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2, v3));
+        *(uint2 *)(smem + off) = make_uint2(pack_relu_bf16x2(v0, v1), pack_relu_bf16x2(v2, v3));
     }
 }
 
@@ -238,10 +318,10 @@ __device__ __forceinline__ void epilogue_act(uint8_t *smem, const Geo<Plan<W, 4>
 // hold at bit col*7+row the value of that cell's (dh,dw) neighbour, so lane
 // element j of a position is bit (col*7+row) of N[s][8q+j].  FROM_X path
 // (Net::forward on arbitrary inputs): gather the fp32 input tensor.
-template <int W, bool FROM_X>
+template <int W, int NPT, bool FROM_X>
 __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const float *__restrict__ x, int base_slot,
                                      int valid, int lane) {
-    using PL = Plan<W, 4>;
+    using PL = Plan<W, 4, NPT>;
     constexpr int NT = PL::NT;
     const int col = lane & 15, q = lane >> 4;
     uint4 a[4];
@@ -250,7 +330,7 @@ __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const fl
     uint4 bv[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        const int p = (PL::T0 + t) * 16 + col;
+        const int p = PL::gpt(t) * 16 + col;
         const int s = p / c4::kCells, cell = p - s * c4::kCells;
         const int h = cell / c4::kCols, wc = cell - h * c4::kCols;
         uint16_t e[8];
@@ -294,52 +374,65 @@ __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const fl
         acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[PL::co(i)]), as_bf16x8(bv[PL::pt(i)]),
                                                         b4[PL::co(i)], 0, 0, 0);
     Geo<NT> g;
-    make_geo<W, 4>(lane, g);
-    epilogue_act<W, kX, false>(smem, g, acc);
+    make_geo<W, 4, NPT>(lane, g);
+    epilogue_act<W, NPT, kX, false>(smem, g, acc);
 }
 
-template <int W>
+template <int W, int S>
 __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, int lane) {
-    using PL = Plan<W, kHeadCT>;
+    constexpr int NPT = npt_of(S);
+    using PL = Plan<W, kHeadCT, NPT>;
     Geo<PL::NT> g;
-    make_geo<W, kHeadCT>(lane, g);
+    make_geo<W, kHeadCT, NPT>(lane, g);
     f32x4 acc[PL::n];
-    uint4 A[3][kHeadCT];
-    load_a01<kHeadCT>(P.w_head, lane, A);
-    conv_mfma<W, kHeadCT, kX>(smem, g, (const float *)(smem + kBias) + kHid * (1 + 2 * P.blocks), P.w_head, nullptr,
+    constexpr int DA = a_depth(S), DB = b_depth(S);
+    uint4 A[DA][PL::CTL];
+    load_a_first<kHeadCT, PL::C0, PL::CTL, DA>(P.w_head, lane, A);
+    conv_mfma<W, kHeadCT, NPT, kX, DA, DB>(smem, g, (const float *)(smem + kBias) + kHid * (1 + 2 * P.blocks), P.w_head, P.w_head,
                               lane, A, acc);
     const int col = lane & 15, q = lane >> 4;
     uint16_t *H = (uint16_t *)(smem + kH);
 #pragma unroll
     for (int i = 0; i < PL::n; ++i) {
         const int co0 = PL::co(i) * 16 + 4 * q;
-        const int p = (PL::T0 + PL::pt(i)) * 16 + col;
+        const int p = PL::gpt(PL::pt(i)) * 16 + col;
         const int s = p / c4::kCells, cell = p - s * c4::kCells;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int co = co0 + r;
-            if (co < kHeadC)
+            if (co < kHeadC && (NPT * 16 == S * c4::kCells || s < S))
                 H[s * kLinK + co * c4::kCells + cell] = __builtin_bit_cast(uint16_t, (__bf16)fmaxf(acc[i][r], 0.f));
         }
     }
-    if (W == 0 && lane < kS * 2) H[(lane >> 1) * kLinK + kHeadC * c4::kCells + (lane & 1)] = 0;   // K padding
+    if (W == 0 && lane < S * 2) H[(lane >> 1) * kLinK + kHeadC * c4::kCells + (lane & 1)] = 0;   // K padding
 }
 
 // fused policy|value linear on MFMA: out[s][o] = sum_k H[s][k] * Wl[o][k]
 // (o < 7 policy logits over k < 1344, o = 7 value pre-activation over
 // 1344 <= k < 1470; connect_four.rs:63-64,69-70).  Wave W takes k-steps
-// [12W, 12W+12) of 46; partial sums go to LDS.
+// [12W, 12W+12) of 46 (weights prefetched by load_lin before the head conv);
+// partial sums go to LDS.
+constexpr int kLinPerWave = 12;
 template <int W>
-__device__ __forceinline__ void linear_mfma(uint8_t *smem, const NetParams &P, int lane) {
-    constexpr int k0 = 12 * W, k1 = (12 * (W + 1) < kLinKSteps) ? 12 * (W + 1) : kLinKSteps;
+__device__ __forceinline__ void load_lin(const NetParams &P, int lane, uint4 (&wl)[kLinPerWave]) {
+    constexpr int k0 = kLinPerWave * W;
+#pragma unroll
+    for (int i = 0; i < kLinPerWave; ++i)
+        if (k0 + i < kLinKSteps) wl[i] = P.w_lin[(k0 + i) * 64 + lane];
+}
+
+template <int W, int S>
+__device__ __forceinline__ void linear_mfma(uint8_t *smem, const uint4 (&wl)[kLinPerWave], int lane) {
+    constexpr int k0 = kLinPerWave * W;
+    constexpr int k1 = (kLinPerWave * (W + 1) < kLinKSteps) ? kLinPerWave * (W + 1) : kLinKSteps;
     const int s = lane & 15, q = lane >> 4;
-    const uint8_t *hrow = s < kS ? smem + kH + s * kLinK * 2 + q * 16 : smem + kZ + q * 16;
-    const int hstep = s < kS ? 64 : 0;
+    const uint8_t *hrow = s < S ? smem + kH + s * kLinK * 2 + q * 16 : smem + kZ + q * 16;
+    const int hstep = s < S ? 64 : 0;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = k0; ks < k1; ++ks) {
         const uint4 a = *(const uint4 *)(hrow + ks * hstep);
-        const uint4 b = P.w_lin[ks * 64 + lane];
+        const uint4 b = wl[ks - k0];
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(b), acc, 0, 0, 0);
     }
     float *L = (float *)(smem + kL) + W * 64;   // D[row s = 4q + r][col o = lane & 15]
@@ -349,129 +442,197 @@ __device__ __forceinline__ void linear_mfma(uint8_t *smem, const NetParams &P, i
     }
 }
 
-template <int W, bool FROM_X>
+template <int W, int S, bool FROM_X>
 __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &P, const float *__restrict__ x,
                                                 int base, int valid, int lane) {
+    constexpr int NPT = npt_of(S);
+    using PL4 = Plan<W, 4, NPT>;
     constexpr size_t kLayer = (size_t)kKStepsRes * 4 * 64;
     const float *bias = (const float *)(smem + kBias);
-    uint4 A[3][4];
-    if (P.blocks > 0) load_a01<4>(P.w_res, lane, A);
-    stem<W, FROM_X>(smem, P, x, base, valid, lane);
-    Geo<Plan<W, 4>::NT> g;
-    make_geo<W, 4>(lane, g);
+    constexpr int DA = a_depth(S), DB = b_depth(S);
+    uint4 A[DA][PL4::CTL];
+    if (P.blocks > 0) load_a_first<4, PL4::C0, PL4::CTL, DA>(P.w_res, lane, A);
+    stem<W, NPT, FROM_X>(smem, P, x, base, valid, lane);
+    Geo<Plan<W, 4, NPT>::NT> g;
+    make_geo<W, 4, NPT>(lane, g);
     __syncthreads();
     stamp(P, W, lane, 1);
     for (int b = 0; b < P.blocks; ++b) {   // relu(x + BN(conv(relu(BN(conv(x)))))), model/mod.rs:152-165
-        f32x4 acc[Plan<W, 4>::n];
+        f32x4 acc[Plan<W, 4, NPT>::n];
         const int l1 = 2 * b, l2 = 2 * b + 1;
-        conv_mfma<W, 4, kX>(smem, g, bias + kHid * (1 + l1), P.w_res + l1 * kLayer, P.w_res + l2 * kLayer, lane, A, acc);
-        epilogue_act<W, kY, false>(smem, g, acc);
+        conv_mfma<W, 4, NPT, kX, DA, DB>(smem, g, bias + kHid * (1 + l1), P.w_res + l1 * kLayer, P.w_res + l2 * kLayer, lane, A, acc);
+#ifdef SPAI_DIAG
+        if (b == 0) {   // make the k-loop's results visible before the stamp
+            asm volatile("" ::"v"(acc[0][0]), "v"(acc[PL4::n - 1][3]));
+            stamp(P, W, lane, 17);
+        }
+#endif
+        epilogue_act<W, NPT, kY, false>(smem, g, acc);
+#ifdef SPAI_DIAG
+        if (b == 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            stamp(P, W, lane, 18);
+        }
+#endif
         __syncthreads();
+#ifdef SPAI_DIAG
+        if (b == 0) stamp(P, W, lane, 19);
+#endif
         if (l1 < 12) stamp(P, W, lane, 2 + l1);
-        conv_mfma<W, 4, kY>(smem, g, bias + kHid * (1 + l2), P.w_res + l2 * kLayer,
-                            b + 1 < P.blocks ? P.w_res + (l2 + 1) * kLayer : nullptr, lane, A, acc);
-        epilogue_act<W, kX, true>(smem, g, acc);
+        conv_mfma<W, 4, NPT, kY, DA, DB>(smem, g, bias + kHid * (1 + l2), P.w_res + l2 * kLayer,
+                            b + 1 < P.blocks ? P.w_res + (l2 + 1) * kLayer : P.w_res + l2 * kLayer, lane, A, acc);
+        epilogue_act<W, NPT, kX, true>(smem, g, acc);
         __syncthreads();
         if (l2 < 12) stamp(P, W, lane, 2 + l2);
     }
-    head_layer<W>(smem, P, lane);
+    uint4 wl[kLinPerWave];
+    load_lin<W>(P, lane, wl);
+    head_layer<W, S>(smem, P, lane);
     __syncthreads();
     stamp(P, W, lane, 14);
-    linear_mfma<W>(smem, P, lane);
+    linear_mfma<W, S>(smem, wl, lane);
 }
 
+template <int S, bool FROM_X>
+__device__ __forceinline__ void run_group(uint8_t *smem, const NetParams &P, const float *__restrict__ x, int base,
+                                          int valid, int wave, int lane) {
+    switch (wave) {
+    case 0: torso_and_heads<0, S, FROM_X>(smem, P, x, base, valid, lane); break;
+    case 1: torso_and_heads<1, S, FROM_X>(smem, P, x, base, valid, lane); break;
+    case 2: torso_and_heads<2, S, FROM_X>(smem, P, x, base, valid, lane); break;
+    default: torso_and_heads<3, S, FROM_X>(smem, P, x, base, valid, lane); break;
+    }
+}
+
+// Group size for `count` leaves on `grid` workgroups: the fewest rounds R of at
+// most kS positions per workgroup, then the smallest S that still fits R rounds
+// (a group's latency grows with its npt_of(S) position tiles, so e.g. 3000
+// leaves run as 2 rounds of S = 6 (16 tiles), not 2 rounds of S = 8 (21 tiles)).
+__host__ __device__ inline int group_size(uint32_t count, uint32_t grid) {
+    const uint32_t cap = grid * (uint32_t)kS;
+    const uint32_t rounds = count ? (count + cap - 1) / cap : 1u;
+    const uint32_t per = grid * rounds;
+    const int g = (int)((count + per - 1) / per);
+    return g < 1 ? 1 : g > kS ? kS : g;
+}
+
+// Persistent forward: the grid is at most one workgroup per CU; each workgroup
+// loops over groups of S positions (S from the device-side leaf count, see
+// group_size; FROM_X and the diagnostic mode use S = force_s).
 template <bool FROM_X>
 __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict__ count_ptr, uint32_t count_imm,
-                                                      const uint64_t *__restrict__ mine, const uint64_t *__restrict__ theirs,
-                                                      const float *__restrict__ x, NetParams P, float *__restrict__ priors,
+                                                      int force_s, const uint64_t *__restrict__ mine,
+                                                      const uint64_t *__restrict__ theirs, const float *__restrict__ x,
+                                                      NetParams P, float *__restrict__ priors,
                                                       float *__restrict__ value, float *__restrict__ logits) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
     const uint32_t count = count_ptr ? *count_ptr : count_imm;
-    const int base = blockIdx.x * kS;
-    if (base >= (int)count) return;
-    const int valid = min(kS, (int)count - base);
+    const int S = force_s > 0 ? force_s : group_size(count, gridDim.x);
+    const int ngroups = (int)((count + S - 1) / S);
+    if ((int)blockIdx.x >= ngroups) return;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
     if (tid < 64) ((uint32_t *)(smem + kZ))[tid] = 0u;
     else if (tid < 128) ((uint32_t *)(smem + kZ1))[tid - 64] = 0u;
-    if (tid < kS) {
-        uint64_t m = 0, t = 0;
-        if (!FROM_X && tid < valid) {
-            m = mine[base + tid];
-            t = theirs[base + tid];
-        }
-        ((uint64_t *)(smem + kB))[2 * tid] = m;
-        ((uint64_t *)(smem + kB))[2 * tid + 1] = t;
-    }
-    if (!FROM_X) {   // neighbour planes N[s][k]: k = tap*3 + plane, shifted so bit b = value at b's neighbour
-        const int s = tid >> 5, k = tid & 31;
-        uint64_t v = 0;
-        if (k < 27 && s < valid) {
-            const uint64_t m = mine[base + s], t = theirs[base + s];
-            const int tap = k / 3, ch = k - tap * 3;
-            const uint64_t plane = ch == 0 ? m : ch == 1 ? t : (~(m | t) & c4::kBoard);
-            const int off = (tap % 3 - 1) * 7 + (tap / 3 - 1);
-            v = off >= 0 ? plane >> off : plane << -off;
-        }
-        ((uint64_t *)(smem + kPlanes))[s * 32 + k] = v;
-    }
     {
         float *bias = (float *)(smem + kBias);
         const int nres = 2 * P.blocks * kHid;
         for (int i = tid; i < kHid + nres + 48; i += kThreads)
             bias[i] = i < kHid ? P.b_stem[i] : i < kHid + nres ? P.b_res[i - kHid] : P.b_head[i - kHid - nres];
     }
-    __syncthreads();
-    stamp(P, wave, lane, 0);
-
-    switch (wave) {
-    case 0: torso_and_heads<0, FROM_X>(smem, P, x, base, valid, lane); break;
-    case 1: torso_and_heads<1, FROM_X>(smem, P, x, base, valid, lane); break;
-    case 2: torso_and_heads<2, FROM_X>(smem, P, x, base, valid, lane); break;
-    default: torso_and_heads<3, FROM_X>(smem, P, x, base, valid, lane); break;
-    }
-    __syncthreads();
-    stamp(P, wave, lane, 15);
-    if (tid < valid) {
-        const float *L = (const float *)(smem + kL);
-        const int slot = base + tid;
-        float sum8[8];
-#pragma unroll
-        for (int o = 0; o < 8; ++o)
-            sum8[o] = L[tid * 8 + o] + L[64 + tid * 8 + o] + L[128 + tid * 8 + o] + L[192 + tid * 8 + o];
-        float lg[c4::kActions];
-        float mx = -INFINITY;
-#pragma unroll
-        for (int a = 0; a < c4::kActions; ++a) {
-            lg[a] = sum8[a] + P.b_pol[a];
-            mx = fmaxf(mx, lg[a]);
+    for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+        const int base = grp * S;
+        const int valid = min(S, (int)count - base);
+        if (tid < kS) {
+            uint64_t m = 0, t = 0;
+            if (!FROM_X && tid < valid) {
+                m = mine[base + tid];
+                t = theirs[base + tid];
+            }
+            ((uint64_t *)(smem + kB))[2 * tid] = m;
+            ((uint64_t *)(smem + kB))[2 * tid + 1] = t;
         }
-        const float v = tanhf(sum8[7] + P.b_val[0]);
-        value[slot] = v;
-        if (logits) {
-#pragma unroll
-            for (int a = 0; a < c4::kActions; ++a) logits[(size_t)slot * c4::kActions + a] = lg[a];
+        if (!FROM_X) {   // neighbour planes N[s][k]: k = tap*3 + plane, shifted so bit b = value at b's neighbour
+            const int s = tid >> 5, k = tid & 31;
+            uint64_t v = 0;
+            if (k < 27 && s < valid) {
+                const uint64_t m = mine[base + s], t = theirs[base + s];
+                const int tap = k / 3, ch = k - tap * 3;
+                const uint64_t plane = ch == 0 ? m : ch == 1 ? t : (~(m | t) & c4::kBoard);
+                const int off = (tap % 3 - 1) * 7 + (tap / 3 - 1);
+                v = off >= 0 ? plane >> off : plane << -off;
+            }
+            ((uint64_t *)(smem + kPlanes))[s * 32 + k] = v;
         }
-        if (priors) {
-            float e[c4::kActions], sum = 0.f;
+        __syncthreads();
+        stamp(P, wave, lane, 0);
+        // hide the lane id from loop-invariant code motion: hoisting the per-lane
+        // geometry out of the group loop would keep it live across every layer
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        ln &= 63;   // restore the known range for the compiler
+        if constexpr (FROM_X) {
+            run_group<kS, true>(smem, P, x, base, valid, wave, ln);
+        } else {
+#ifdef SPAI_ONLY_S
+            run_group<SPAI_ONLY_S, false>(smem, P, x, base, valid, wave, ln);
+#else
+            switch (S) {
+            case 1: run_group<1, false>(smem, P, x, base, valid, wave, ln); break;
+            case 2: run_group<2, false>(smem, P, x, base, valid, wave, ln); break;
+            case 3: run_group<3, false>(smem, P, x, base, valid, wave, ln); break;
+            case 4: run_group<4, false>(smem, P, x, base, valid, wave, ln); break;
+            case 5: run_group<5, false>(smem, P, x, base, valid, wave, ln); break;
+            case 6: run_group<6, false>(smem, P, x, base, valid, wave, ln); break;
+            case 7: run_group<7, false>(smem, P, x, base, valid, wave, ln); break;
+            default: run_group<8, false>(smem, P, x, base, valid, wave, ln); break;
+            }
+#endif
+        }
+        __syncthreads();
+        stamp(P, wave, lane, 15);
+        if (tid < valid) {
+            const float *L = (const float *)(smem + kL);
+            const int slot = base + tid;
+            float sum8[8];
+#pragma unroll
+            for (int o = 0; o < 8; ++o)
+                sum8[o] = L[tid * 8 + o] + L[64 + tid * 8 + o] + L[128 + tid * 8 + o] + L[192 + tid * 8 + o];
+            float lg[c4::kActions];
+            float mx = -INFINITY;
 #pragma unroll
             for (int a = 0; a < c4::kActions; ++a) {
-                e[a] = __expf(lg[a] - mx);
-                sum += e[a];
+                lg[a] = sum8[a] + P.b_pol[a];
+                mx = fmaxf(mx, lg[a]);
             }
-            const float inv = 1.0f / sum;
+            const float v = tanhf(sum8[7] + P.b_val[0]);
+            value[slot] = v;
+            if (logits) {
 #pragma unroll
-            for (int a = 0; a < c4::kActions; ++a) e[a] *= inv;
-            const uint64_t *bb = (const uint64_t *)(smem + kB);
-            float out[c4::kActions];
-            c4::mask_renorm(e, c4::open_columns(bb[2 * tid] | bb[2 * tid + 1]), out);
-            float4 *pr = (float4 *)(priors + (size_t)slot * kPriorStride);
-            pr[0] = make_float4(out[0], out[1], out[2], out[3]);
-            pr[1] = make_float4(out[4], out[5], out[6], 0.f);
+                for (int a = 0; a < c4::kActions; ++a) logits[(size_t)slot * c4::kActions + a] = lg[a];
+            }
+            if (priors) {
+                float e[c4::kActions], sum = 0.f;
+#pragma unroll
+                for (int a = 0; a < c4::kActions; ++a) {
+                    e[a] = __expf(lg[a] - mx);
+                    sum += e[a];
+                }
+                const float inv = 1.0f / sum;
+#pragma unroll
+                for (int a = 0; a < c4::kActions; ++a) e[a] *= inv;
+                const uint64_t *bb = (const uint64_t *)(smem + kB);
+                float out[c4::kActions];
+                c4::mask_renorm(e, c4::open_columns(bb[2 * tid] | bb[2 * tid + 1]), out);
+                float4 *pr = (float4 *)(priors + (size_t)slot * kPriorStride);
+                pr[0] = make_float4(out[0], out[1], out[2], out[3]);
+                pr[1] = make_float4(out[4], out[5], out[6], 0.f);
+            }
         }
+        stamp(P, wave, lane, 16);
+        __syncthreads();   // kB / planes / L are rewritten by the next group
     }
-    stamp(P, wave, lane, 16);
 }
 
 // ---------------------------------------------------------------- host packing
@@ -587,6 +748,8 @@ int net_create(spai_engine *e, int blocks, int hidden, const float *params, size
 
     spai_net *n = new spai_net();
     n->eng = e;
+    if (hipDeviceGetAttribute(&n->n_cu, hipDeviceAttributeMultiprocessorCount, e->device) != hipSuccess || n->n_cu < 1)
+        n->n_cu = 256;
     n->blocks = blocks;
     n->hidden = hidden;
     int rc = SPAI_OK;
@@ -670,6 +833,11 @@ int ensure_io(spai_net *n, uint32_t cnt) {
 }
 
 int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
+#ifndef SPAI_DIAG
+    (void)n;
+    (void)cycles;
+    SPAI_CHECK(false, SPAI_ERR_UNSUPPORTED, "phase stamps need the diagnostic build (make -C self-play-ai_amd diag)");
+#endif
     SPAI_CHECK(cnt > 0, SPAI_ERR_INVALID, "need cnt > 0");
     SPAI_TRY(ensure_io(n, cnt));
     hipStream_t st = n->eng->stream;
@@ -690,7 +858,9 @@ int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
         m[i] = xm ? s.x : s.o;
         t[i] = xm ? s.o : s.x;
     }
-    const uint32_t grid = (cnt + kS - 1) / kS;
+    const char *es = std::getenv("SPAI_PHASE_S");   // diagnostic: group size to time (default 8)
+    const int S = es ? std::max(1, std::min(kS, std::atoi(es))) : kS;
+    const uint32_t grid = (cnt + S - 1) / S;
     DevBuf<unsigned long long> d;
     SPAI_TRY(d.alloc((size_t)grid * kWaves * kStamps));
     SPAI_HIP(hipMemsetAsync(d.p, 0, d.n * 8, st));
@@ -699,7 +869,7 @@ int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
     NetParams P = params_of(n);
     P.stamps = d.p;
     for (int rep = 0; rep < 3; ++rep)   // last launch warm
-        k_forward<false><<<grid, kThreads, 0, st>>>(nullptr, cnt, n->io_mine.p, n->io_theirs.p, nullptr, P,
+        k_forward<false><<<grid, kThreads, 0, st>>>(nullptr, cnt, S, n->io_mine.p, n->io_theirs.p, nullptr, P,
                                                    n->io_priors.p, n->io_value.p, nullptr);
     SPAI_HIP(hipGetLastError());
     std::vector<unsigned long long> hs(d.n);
@@ -711,7 +881,7 @@ int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
     for (uint32_t g = 0; g < grid; ++g)
         for (int w = 0; w < kWaves; ++w) {
             const unsigned long long *sp = hs.data() + ((size_t)g * kWaves + w) * kStamps;
-            if (!sp[0] || !sp[16]) continue;
+            if (!sp[0] || !sp[16]) continue;   // (a workgroup with no group)
             for (int k = 0; k < kStamps; ++k) cycles[k] += sp[k] ? (double)(sp[k] - sp[0]) : 0.0;
             cntw += 1;
         }
@@ -722,9 +892,9 @@ int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
 int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint32_t max_n, const uint64_t *mine,
                    const uint64_t *theirs, float *priors, float *value) {
     if (!max_n) return SPAI_OK;
-    const uint32_t grid = (max_n + kS - 1) / kS;
-    k_forward<false><<<grid, kThreads, 0, st>>>(d_count, max_n, mine, theirs, nullptr, params_of(net), priors, value,
-                                                nullptr);
+    const uint32_t grid = std::min<uint32_t>(max_n, (uint32_t)net->n_cu);
+    k_forward<false><<<grid, kThreads, 0, st>>>(d_count, max_n, 0, mine, theirs, nullptr, params_of(net), priors,
+                                                value, nullptr);
     SPAI_HIP(hipGetLastError());
     return SPAI_OK;
 }
@@ -735,8 +905,8 @@ int net_forward_x(spai_net *n, uint32_t cnt, const float *x, float *logits, floa
     SPAI_TRY(ensure_io(n, cnt));
     hipStream_t st = n->eng->stream;
     SPAI_HIP(hipMemcpyAsync(n->io_x.p, x, (size_t)cnt * 126 * 4, hipMemcpyHostToDevice, st));
-    k_forward<true><<<(cnt + kS - 1) / kS, kThreads, 0, st>>>(nullptr, cnt, nullptr, nullptr, n->io_x.p, params_of(n),
-                                                             nullptr, n->io_value.p, n->io_logits.p);
+    k_forward<true><<<(cnt + kS - 1) / kS, kThreads, 0, st>>>(nullptr, cnt, kS, nullptr, nullptr, n->io_x.p,
+                                                             params_of(n), nullptr, n->io_value.p, n->io_logits.p);
     SPAI_HIP(hipGetLastError());
     SPAI_HIP(hipMemcpyAsync(logits, n->io_logits.p, (size_t)cnt * 28, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipMemcpyAsync(value, n->io_value.p, (size_t)cnt * 4, hipMemcpyDeviceToHost, st));
@@ -756,8 +926,8 @@ int net_predict(spai_net *n, uint32_t cnt, const spai_c4_state *states, float *p
     hipStream_t st = n->eng->stream;
     SPAI_HIP(hipMemcpyAsync(n->io_mine.p, m.data(), (size_t)cnt * 8, hipMemcpyHostToDevice, st));
     SPAI_HIP(hipMemcpyAsync(n->io_theirs.p, t.data(), (size_t)cnt * 8, hipMemcpyHostToDevice, st));
-    k_forward<false><<<(cnt + kS - 1) / kS, kThreads, 0, st>>>(nullptr, cnt, n->io_mine.p, n->io_theirs.p, nullptr,
-                                                              params_of(n), n->io_priors.p, n->io_value.p, nullptr);
+    k_forward<false><<<std::min<uint32_t>(cnt, (uint32_t)n->n_cu), kThreads, 0, st>>>(
+        nullptr, cnt, 0, n->io_mine.p, n->io_theirs.p, nullptr, params_of(n), n->io_priors.p, n->io_value.p, nullptr);
     SPAI_HIP(hipGetLastError());
     std::vector<float> pr((size_t)cnt * kPriorStride);
     SPAI_HIP(hipMemcpyAsync(pr.data(), n->io_priors.p, pr.size() * 4, hipMemcpyDeviceToHost, st));

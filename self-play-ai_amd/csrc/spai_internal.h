@@ -115,6 +115,7 @@ struct KernelTimer {
 struct spai_net {
     spai_engine *eng = nullptr;
     int blocks = 0, hidden = 0;
+    int n_cu = 256;                 // compute units: the persistent forward's grid
     // packed, BN-folded bf16 MFMA fragments + fp32 biases / head linears (see net_c4.hip)
     spai::DevBuf<uint16_t> w_stem, w_res, w_head, w_lin;
     spai::DevBuf<float> b_stem, b_res, b_head, b_pol, b_val;

@@ -14,7 +14,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libspai.so")
+LIB_PATH = os.environ.get("SPAI_LIB") or os.path.join(HERE, "libspai.so")
 
 GAME_TICTACTOE, GAME_CONNECT4, GAME_CHESS = 0, 1, 2
 EVAL_NET, EVAL_UNIFORM, EVAL_HASH = 0, 1, 2
@@ -178,7 +178,7 @@ class Net:
         return lg, v
 
     def phase_cycles(self, count=4096):
-        c = np.zeros(17, np.float64)
+        c = np.zeros(20, np.float64)
         _check(lib().spai_net_phase_cycles(self.h, count, _p(c)))
         return c
 
