@@ -145,11 +145,15 @@ int spai_engine_create(int game, const spai_config *cfg, int device, spai_engine
     e->game = game;
     e->device = device;
     e->cfg = *cfg;
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess || e->err.alloc(1) != SPAI_OK) {
+    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&e->chain_stream[1], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess || e->err.alloc(1) != SPAI_OK) {
         set_error("engine stream / scratch allocation failed");
         delete e;
         return SPAI_ERR_DEVICE;
     }
+    e->chain_stream[0] = e->stream;
     *out = e;
     return SPAI_OK;
 }
@@ -168,14 +172,15 @@ int spai_engine_destroy(spai_engine *e) {
     T.root_status.release();
     T.path.release();
     T.depth.release();
-    Batch &B = e->batch;
-    B.count.release();
-    B.tree.release();
-    B.mine.release();
-    B.theirs.release();
-    B.priors.release();
-    B.value.release();
-    B.iter_counts.release();
+    for (Batch &B : e->batch) {
+        B.count.release();
+        B.tree.release();
+        B.mine.release();
+        B.theirs.release();
+        B.priors.release();
+        B.value.release();
+        B.iter_counts.release();
+    }
     e->games.x.release();
     e->games.o.release();
     e->games.n.release();
@@ -184,6 +189,10 @@ int spai_engine_destroy(spai_engine *e) {
     e->err.release();
     e->stats.release();
     for (hipEvent_t ev : e->timer.ev) (void)hipEventDestroy(ev);
+    if (e->chain_stream[1]) (void)hipStreamSynchronize(e->chain_stream[1]);
+    if (e->chain_stream[1]) (void)hipStreamDestroy(e->chain_stream[1]);
+    if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     (void)hipStreamDestroy(e->stream);
     delete e;
     return SPAI_OK;

@@ -241,9 +241,20 @@ TreeView tree_view(spai_engine *e) {
                     T.path.p, T.depth.p};
 }
 
-BatchView batch_view(spai_engine *e, uint32_t slot) {
-    Batch &B = e->batch;
+BatchView batch_view(spai_engine *e, int chain, uint32_t slot) {
+    Batch &B = e->batch[chain];
     return BatchView{B.count.p + slot, B.tree.p, B.mine.p, B.theirs.p, B.priors.p, B.value.p};
+}
+
+// Number of search chains for n trees: two halves when each half still fills
+// a useful batch (SPAI_CHAINS=1 forces one chain, for A/B measurements).
+int chains_for(uint32_t n) {
+    static const int forced = [] {
+        const char *v = std::getenv("SPAI_CHAINS");
+        return v ? std::atoi(v) : 0;
+    }();
+    if (forced == 1) return 1;
+    return n >= 128 ? spai_engine::kChains : 1;
 }
 
 // upload host root bookkeeping for trees [t0, t0+n)
@@ -330,14 +341,15 @@ int trees_create(spai_engine *e, uint32_t n) {
         SPAI_TRY(T.depth.alloc(n));
         SPAI_TRY(e->active.alloc(n));
         SPAI_TRY(e->stats.alloc((size_t)n * 8));
-        Batch &B = e->batch;
-        SPAI_TRY(B.count.alloc(2));
-        SPAI_TRY(B.tree.alloc(n));
-        SPAI_TRY(B.mine.alloc(n));
-        SPAI_TRY(B.theirs.alloc(n));
-        SPAI_TRY(B.priors.alloc((size_t)n * kPriorStride));
-        SPAI_TRY(B.value.alloc(n));
-        B.cap = n;
+        for (Batch &B : e->batch) {   // one leaf batch per search chain
+            SPAI_TRY(B.count.alloc(2));
+            SPAI_TRY(B.tree.alloc(n));
+            SPAI_TRY(B.mine.alloc(n));
+            SPAI_TRY(B.theirs.alloc(n));
+            SPAI_TRY(B.priors.alloc((size_t)n * kPriorStride));
+            SPAI_TRY(B.value.alloc(n));
+            B.cap = n;
+        }
         T.n_trees = n;
         T.cap = (uint32_t)cap;
     }
@@ -378,43 +390,72 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
     SPAI_CHECK(kind != SPAI_EVAL_NET || e->net, SPAI_ERR_INVALID, "eval = NET but no net set (spai_engine_set_net)");
     if (n == 0) return SPAI_OK;
     hipStream_t st = e->stream;
-    Batch &B = e->batch;
-    if (B.iter_counts.n < num_searches) SPAI_TRY(B.iter_counts.alloc(std::max<uint32_t>(num_searches, 1)));
+    // chain h searches active[off[h] .. off[h] + cnt[h]) on chain_stream[h]
+    const int nchain = chains_for(n);
+    uint32_t off[spai_engine::kChains] = {0, 0}, cnt[spai_engine::kChains] = {n, 0};
+    if (nchain == 2) {
+        cnt[0] = (n + 1) / 2;
+        off[1] = cnt[0];
+        cnt[1] = n - cnt[0];
+    }
+    for (int h = 0; h < nchain; ++h) {
+        Batch &B = e->batch[h];
+        if (B.iter_counts.n < num_searches) SPAI_TRY(B.iter_counts.alloc(std::max<uint32_t>(num_searches, 1)));
+        SPAI_HIP(hipMemsetAsync(B.count.p, 0, 8, st));
+    }
     SPAI_HIP(hipMemcpyAsync(e->active.p, tree_idx, n * 4, hipMemcpyHostToDevice, st));
     SPAI_HIP(hipMemsetAsync(e->err.p, 0, 4, st));
-    SPAI_HIP(hipMemsetAsync(B.count.p, 0, 8, st));
+    if (nchain == 2) {   // fork: chain 1 starts after the setup on the engine stream
+        SPAI_HIP(hipEventRecord(e->ev_fork, st));
+        SPAI_HIP(hipStreamWaitEvent(e->chain_stream[1], e->ev_fork, 0));
+    }
     const TreeView tv = tree_view(e);
-    const uint32_t g8 = (n + kTreesPerBlock - 1) / kTreesPerBlock;
-    const bool timed = e->timer.enabled;
+    const bool timed = e->timer.enabled;   // samples chain 0's launches
     for (uint32_t it = 0; it < num_searches; ++it) {
-        const bool sample = timed && (it % 4 == 0);
         const uint32_t cur = it & 1u;
-        const BatchView bv = batch_view(e, cur);
-        if (sample) SPAI_TRY(timer_record(e, 0, it, true));
-        k_select<<<g8, kBlock, 0, st>>>(tv, bv, e->active.p, n, e->cfg.c, e->err.p);
-        if (sample) SPAI_TRY(timer_record(e, 0, it, false));
-        if (sample) SPAI_TRY(timer_record(e, 1, it, true));
-        if (kind == SPAI_EVAL_NET) {
-            SPAI_TRY(net_eval_batch(e->net, st, bv.count, n, B.mine.p, B.theirs.p, B.priors.p, B.value.p));
-        } else {
-            k_eval_stub<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(bv, n, kind);
+        for (int h = 0; h < nchain; ++h) {
+            const hipStream_t sh = e->chain_stream[h];
+            Batch &B = e->batch[h];
+            const BatchView bv = batch_view(e, h, cur);
+            const uint32_t nh = cnt[h], g8 = (nh + kTreesPerBlock - 1) / kTreesPerBlock;
+            const uint32_t *act = e->active.p + off[h];
+            const bool sample = timed && h == 0 && (it % 4 == 0);
+            if (sample) SPAI_TRY(timer_record(e, 0, it, true));
+            k_select<<<g8, kBlock, 0, sh>>>(tv, bv, act, nh, e->cfg.c, e->err.p);
+            if (sample) SPAI_TRY(timer_record(e, 0, it, false));
+            if (sample) SPAI_TRY(timer_record(e, 1, it, true));
+            if (kind == SPAI_EVAL_NET) {
+                SPAI_TRY(net_eval_batch(e->net, sh, bv.count, nh, B.mine.p, B.theirs.p, B.priors.p, B.value.p));
+            } else {
+                k_eval_stub<<<(nh + kBlock - 1) / kBlock, kBlock, 0, sh>>>(bv, nh, kind);
+            }
+            if (sample) SPAI_TRY(timer_record(e, 1, it, false));
+            if (sample) SPAI_TRY(timer_record(e, 2, it, true));
+            k_expand<<<g8, kBlock, 0, sh>>>(tv, bv, nh, e->err.p, B.iter_counts.p + it, B.count.p + (cur ^ 1u));
+            if (sample) SPAI_TRY(timer_record(e, 2, it, false));
         }
-        if (sample) SPAI_TRY(timer_record(e, 1, it, false));
-        if (sample) SPAI_TRY(timer_record(e, 2, it, true));
-        k_expand<<<g8, kBlock, 0, st>>>(tv, bv, n, e->err.p, B.iter_counts.p + it, B.count.p + (cur ^ 1u));
-        if (sample) SPAI_TRY(timer_record(e, 2, it, false));
     }
     SPAI_HIP(hipGetLastError());
+    if (nchain == 2) {   // join
+        SPAI_HIP(hipEventRecord(e->ev_join, e->chain_stream[1]));
+        SPAI_HIP(hipStreamWaitEvent(st, e->ev_join, 0));
+    }
     k_root_stats<<<(n + 255) / 256, 256, 0, st>>>(tv, e->active.p, n, e->stats.p);
     SPAI_HIP(hipGetLastError());
-    std::vector<uint32_t> stats((size_t)n * 8), counts(num_searches);
+    std::vector<uint32_t> stats((size_t)n * 8), counts(num_searches), counts1(num_searches);
     uint32_t err = 0;
     SPAI_HIP(hipMemcpyAsync(stats.data(), e->stats.p, stats.size() * 4, hipMemcpyDeviceToHost, st));
-    if (num_searches)
-        SPAI_HIP(hipMemcpyAsync(counts.data(), B.iter_counts.p, num_searches * 4, hipMemcpyDeviceToHost, st));
+    if (num_searches) {
+        SPAI_HIP(hipMemcpyAsync(counts.data(), e->batch[0].iter_counts.p, num_searches * 4, hipMemcpyDeviceToHost, st));
+        if (nchain == 2)
+            SPAI_HIP(hipMemcpyAsync(counts1.data(), e->batch[1].iter_counts.p, num_searches * 4, hipMemcpyDeviceToHost,
+                                    st));
+    }
     SPAI_HIP(hipMemcpyAsync(&err, e->err.p, 4, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipStreamSynchronize(st));
-    SPAI_TRY(timer_collect(e, counts, n));
+    SPAI_TRY(timer_collect(e, counts, cnt[0]));   // chain 0's launches and items
+    if (nchain == 2)
+        for (uint32_t i = 0; i < num_searches; ++i) counts[i] += counts1[i];
     SPAI_CHECK(!(err & kErrCapacity), SPAI_ERR_CAPACITY, "node arena full (cap %u per tree)", T.cap);
     SPAI_CHECK(!(err & kErrDepth), SPAI_ERR_CAPACITY, "tree deeper than %d", kMaxDepth);
     SPAI_CHECK(!(err & kErrNan), SPAI_ERR_NAN, "NaN UCB in select (reference: partial_cmp().unwrap() panics)");

@@ -131,7 +131,14 @@ struct spai_engine {
     hipStream_t stream = nullptr;
     spai::GameSlots games;
     spai::Trees trees;
-    spai::Batch batch;
+    // The search runs its trees as kChains independent chains (select -> evaluate
+    // -> expand), each with its own batch on its own stream, so one chain's
+    // latency-bound tree kernels overlap the other's forward.  Chain 0 uses
+    // `stream`.
+    static constexpr int kChains = 2;
+    spai::Batch batch[kChains];
+    hipStream_t chain_stream[kChains] = {nullptr, nullptr};
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     spai_net *net = nullptr;
     spai::DevBuf<uint32_t> active;   // active tree list
     spai::DevBuf<uint32_t> err;      // device error flags
