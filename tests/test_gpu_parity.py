@@ -187,7 +187,65 @@ def test_net_partial_batches(spai):
     e.close()
 
 
+def _reachable_positions(spai, n, plies, seed):
+    """ongoing positions after up to `plies` random legal moves (device rules)"""
+    e = spai.Engine(num_searches=1, max_trees=1)
+    rng = np.random.default_rng(seed)
+    e.games_resize(n)
+    for _ in range(plies):
+        lm = e.legal_mask(n)
+        r = rng.random((n, 7)) * ((lm[:, None] >> np.arange(7)) & 1)
+        e.apply(np.argmax(r, 1).astype(np.int32), check=False)
+    st = e.games_read(n)
+    e.close()
+    return [tuple(int(v) for v in (r["x"], r["o"], r["n"], r["status"])) for r in st if r["status"] == 0]
+
+
+def test_net_group_size_invariance(spai):
+    """the persistent forward picks 1..8 positions per workgroup group from the
+    batch size (and three task orders with it); a position's priors and value
+    must not depend on which group size or slot it ran in"""
+    states = _reachable_positions(spai, 2600, 14, seed=9)
+    assert len(states) > 2100
+    e = spai.Engine(num_searches=1, max_trees=1)
+    net = spai.Net(e, 6, spai.init_params(6, 64, seed=2))
+    full_p, full_v = net.predict(states[:2100])      # 2 rounds of S = 5 on 256 CUs
+    for n in (1, 40, 300, 700, 1000, 1300, 1500, 1700, 1800, 2048):   # S = 1..8
+        p, v = net.predict(states[:n])
+        np.testing.assert_array_equal(p, full_p[:n])
+        np.testing.assert_array_equal(v, full_v[:n])
+    p, v = net.predict(states[1000:1003])            # other slots than in the full batch
+    np.testing.assert_array_equal(p, full_p[1000:1003])
+    np.testing.assert_array_equal(v, full_v[1000:1003])
+    net.close()
+    e.close()
+
+
 # ------------------------------------------------------------------ search
+def test_search_chain_split_invariance(spai):
+    """NET search over 200 trees runs as two chains (two streams, two batches);
+    the same first 100 trees searched alone run as one chain and must get
+    bit-identical visit counts"""
+    roots = _reachable_positions(spai, 260, 6, seed=4)[:200]
+    assert len(roots) == 200
+    params = spai.init_params(6, 64, seed=5)
+    out = []
+    for n in (200, 100):
+        e = spai.Engine(num_searches=64, max_trees=n, eval_kind=spai.EVAL_NET, max_moves=2)
+        net = spai.Net(e, 6, params)
+        e.set_net(net)
+        e.trees_create(n)
+        for i in range(n):
+            e.tree_reset(i, roots[i])
+        out.append(e.search(np.arange(n), 64))
+        net.close()
+        e.close()
+    (pa, ia, va, na), (pb, ib, vb, nb) = out
+    np.testing.assert_array_equal(na[:100], nb)
+    np.testing.assert_array_equal(va[:100], vb)
+    np.testing.assert_array_equal(pa[:100], pb)
+
+
 def test_search_hash_matches_oracle(spai, oracle, eng):
     d = json.load(open(os.path.join(GOLDEN, "mcts_hash.json")))
     cases = d["search"]
@@ -209,8 +267,9 @@ def test_search_uniform_first_select(spai):
 
 
 def test_search_batched_with_subtree_reuse(spai, oracle):
-    """many trees searched together, then re-rooted (use_subtree keeps N, W) and searched again"""
-    n, sims = 96, 48
+    """many trees searched together (two search chains), then re-rooted (use_subtree
+    keeps N, W) and searched again"""
+    n, sims = 160, 48
     rng = np.random.default_rng(5)
     roots = []
     for g in range(n):
@@ -260,7 +319,9 @@ def test_search_batched_with_subtree_reuse(spai, oracle):
 
 # ------------------------------------------------------------------ self-play
 def test_self_play_hash_matches_oracle(spai, oracle):
-    n, sims, seed = 64, 32, 11
+    # 160 games: the search runs as two chains (>= 128 active trees) until
+    # enough games finish, then as one, all checked bit-exactly
+    n, sims, seed = 160, 32, 11
     e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_HASH, seed=seed)
     games, stats = e.self_play(n)
     ref = oracle.self_play(oracle.GAME_CONNECT4, n, sims, seed, eval_kind=oracle.EVAL_HASH, max_plies=42)
