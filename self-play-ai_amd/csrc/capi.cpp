@@ -145,10 +145,12 @@ int spai_engine_create(int game, const spai_config *cfg, int device, spai_engine
     e->game = game;
     e->device = device;
     e->cfg = *cfg;
-    if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&e->chain_stream[1], hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming) != hipSuccess || e->err.alloc(1) != SPAI_OK) {
+    bool ok = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming) == hipSuccess && e->err.alloc(1) == SPAI_OK;
+    for (int h = 1; h < spai_engine::kChains && ok; ++h)
+        ok = hipStreamCreateWithFlags(&e->chain_stream[h], hipStreamNonBlocking) == hipSuccess &&
+             hipEventCreateWithFlags(&e->ev_join[h], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
         set_error("engine stream / scratch allocation failed");
         delete e;
         return SPAI_ERR_DEVICE;
@@ -189,10 +191,12 @@ int spai_engine_destroy(spai_engine *e) {
     e->err.release();
     e->stats.release();
     for (hipEvent_t ev : e->timer.ev) (void)hipEventDestroy(ev);
-    if (e->chain_stream[1]) (void)hipStreamSynchronize(e->chain_stream[1]);
-    if (e->chain_stream[1]) (void)hipStreamDestroy(e->chain_stream[1]);
+    for (int h = 1; h < spai_engine::kChains; ++h) {
+        if (e->chain_stream[h]) (void)hipStreamSynchronize(e->chain_stream[h]);
+        if (e->chain_stream[h]) (void)hipStreamDestroy(e->chain_stream[h]);
+        if (e->ev_join[h]) (void)hipEventDestroy(e->ev_join[h]);
+    }
     if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
-    if (e->ev_join) (void)hipEventDestroy(e->ev_join);
     (void)hipStreamDestroy(e->stream);
     delete e;
     return SPAI_OK;

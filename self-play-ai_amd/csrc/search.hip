@@ -247,14 +247,14 @@ BatchView batch_view(spai_engine *e, int chain, uint32_t slot) {
 }
 
 // Number of search chains for n trees: two halves when each half still fills
-// a useful batch (SPAI_CHAINS=1 forces one chain, for A/B measurements).
+// a useful batch (SPAI_CHAINS=k forces up to k chains, for A/B measurements).
 int chains_for(uint32_t n) {
     static const int forced = [] {
         const char *v = std::getenv("SPAI_CHAINS");
-        return v ? std::atoi(v) : 0;
+        return v ? std::max(1, std::min(spai_engine::kChains, std::atoi(v))) : 0;
     }();
-    if (forced == 1) return 1;
-    return n >= 128 ? spai_engine::kChains : 1;
+    const int want = forced ? forced : 2;
+    return std::max(1, std::min<int>(want, (int)(n / 64)));
 }
 
 // upload host root bookkeeping for trees [t0, t0+n)
@@ -392,11 +392,10 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
     hipStream_t st = e->stream;
     // chain h searches active[off[h] .. off[h] + cnt[h]) on chain_stream[h]
     const int nchain = chains_for(n);
-    uint32_t off[spai_engine::kChains] = {0, 0}, cnt[spai_engine::kChains] = {n, 0};
-    if (nchain == 2) {
-        cnt[0] = (n + 1) / 2;
-        off[1] = cnt[0];
-        cnt[1] = n - cnt[0];
+    uint32_t off[spai_engine::kChains] = {0, 0, 0, 0}, cnt[spai_engine::kChains] = {0, 0, 0, 0};
+    for (int h = 0; h < nchain; ++h) {
+        off[h] = (uint32_t)((uint64_t)n * h / nchain);
+        cnt[h] = (uint32_t)((uint64_t)n * (h + 1) / nchain) - off[h];
     }
     for (int h = 0; h < nchain; ++h) {
         Batch &B = e->batch[h];
@@ -405,9 +404,9 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
     }
     SPAI_HIP(hipMemcpyAsync(e->active.p, tree_idx, n * 4, hipMemcpyHostToDevice, st));
     SPAI_HIP(hipMemsetAsync(e->err.p, 0, 4, st));
-    if (nchain == 2) {   // fork: chain 1 starts after the setup on the engine stream
+    if (nchain > 1) {   // fork: chains 1.. start after the setup on the engine stream
         SPAI_HIP(hipEventRecord(e->ev_fork, st));
-        SPAI_HIP(hipStreamWaitEvent(e->chain_stream[1], e->ev_fork, 0));
+        for (int h = 1; h < nchain; ++h) SPAI_HIP(hipStreamWaitEvent(e->chain_stream[h], e->ev_fork, 0));
     }
     const TreeView tv = tree_view(e);
     const bool timed = e->timer.enabled;   // samples chain 0's launches
@@ -436,26 +435,24 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
         }
     }
     SPAI_HIP(hipGetLastError());
-    if (nchain == 2) {   // join
-        SPAI_HIP(hipEventRecord(e->ev_join, e->chain_stream[1]));
-        SPAI_HIP(hipStreamWaitEvent(st, e->ev_join, 0));
+    for (int h = 1; h < nchain; ++h) {   // join
+        SPAI_HIP(hipEventRecord(e->ev_join[h], e->chain_stream[h]));
+        SPAI_HIP(hipStreamWaitEvent(st, e->ev_join[h], 0));
     }
     k_root_stats<<<(n + 255) / 256, 256, 0, st>>>(tv, e->active.p, n, e->stats.p);
     SPAI_HIP(hipGetLastError());
-    std::vector<uint32_t> stats((size_t)n * 8), counts(num_searches), counts1(num_searches);
+    std::vector<uint32_t> stats((size_t)n * 8), counts(num_searches), ch_counts((size_t)nchain * num_searches);
     uint32_t err = 0;
     SPAI_HIP(hipMemcpyAsync(stats.data(), e->stats.p, stats.size() * 4, hipMemcpyDeviceToHost, st));
-    if (num_searches) {
-        SPAI_HIP(hipMemcpyAsync(counts.data(), e->batch[0].iter_counts.p, num_searches * 4, hipMemcpyDeviceToHost, st));
-        if (nchain == 2)
-            SPAI_HIP(hipMemcpyAsync(counts1.data(), e->batch[1].iter_counts.p, num_searches * 4, hipMemcpyDeviceToHost,
-                                    st));
-    }
+    if (num_searches)
+        for (int h = 0; h < nchain; ++h)
+            SPAI_HIP(hipMemcpyAsync(ch_counts.data() + (size_t)h * num_searches, e->batch[h].iter_counts.p,
+                                    num_searches * 4, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipMemcpyAsync(&err, e->err.p, 4, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipStreamSynchronize(st));
-    SPAI_TRY(timer_collect(e, counts, cnt[0]));   // chain 0's launches and items
-    if (nchain == 2)
-        for (uint32_t i = 0; i < num_searches; ++i) counts[i] += counts1[i];
+    SPAI_TRY(timer_collect(e, ch_counts, cnt[0]));   // chain 0's launches and items
+    for (int h = 0; h < nchain; ++h)
+        for (uint32_t i = 0; i < num_searches; ++i) counts[i] += ch_counts[(size_t)h * num_searches + i];
     SPAI_CHECK(!(err & kErrCapacity), SPAI_ERR_CAPACITY, "node arena full (cap %u per tree)", T.cap);
     SPAI_CHECK(!(err & kErrDepth), SPAI_ERR_CAPACITY, "tree deeper than %d", kMaxDepth);
     SPAI_CHECK(!(err & kErrNan), SPAI_ERR_NAN, "NaN UCB in select (reference: partial_cmp().unwrap() panics)");

@@ -135,10 +135,10 @@ struct spai_engine {
     // -> expand), each with its own batch on its own stream, so one chain's
     // latency-bound tree kernels overlap the other's forward.  Chain 0 uses
     // `stream`.
-    static constexpr int kChains = 2;
+    static constexpr int kChains = 4;    // capacity; the search uses chains_for(n) of them
     spai::Batch batch[kChains];
-    hipStream_t chain_stream[kChains] = {nullptr, nullptr};
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipStream_t chain_stream[kChains] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev_fork = nullptr, ev_join[kChains] = {nullptr, nullptr, nullptr, nullptr};
     spai_net *net = nullptr;
     spai::DevBuf<uint32_t> active;   // active tree list
     spai::DevBuf<uint32_t> err;      // device error flags
