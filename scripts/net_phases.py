@@ -19,8 +19,10 @@ for n in (2048, 4096):
 for S in range(1, 9):
     os.environ["SPAI_PHASE_S"] = str(S)
     c = net.phase_cycles(256 * S)
-    print(f"S={S}: {c[16]:.0f} cycles/wave = {c[16] / 2.1e3:.1f} us @2.1GHz  (res layer ~{np.diff(c)[3]:.0f}; "
-          f"block0 conv1: k-loop {c[17] - c[1]:.0f}, epilogue {c[18] - c[17]:.0f}, barrier {c[19] - c[18]:.0f})")
+    d = np.diff(c[:17])
+    print(f"S={S}: {c[16]:.0f} cycles/wave = {c[16] / 2.1e3:.1f} us @2.1GHz  stem {d[0]:.0f} res0 {d[1]:.0f} "
+          f"res1 {d[2]:.0f} res2 {d[3]:.0f} head {d[13]:.0f} linear {d[14]:.0f} end {d[15]:.0f}; "
+          f"block0 conv1: k-loop {c[17] - c[1]:.0f}, epilogue {c[18] - c[17]:.0f}, barrier {c[19] - c[18]:.0f}")
 os.environ.pop("SPAI_PHASE_S")
 net.close()
 e.close()

@@ -67,7 +67,8 @@ constexpr int kMaxBlocks = 20;
 constexpr int kBiasFloats = kHid + 2 * kMaxBlocks * kHid + 48;   // stem, residual convs, head
 constexpr int kBias = kL + kWaves * 64 * 4; // all conv biases, staged once per workgroup
 constexpr int kPlanes = kBias + kBiasFloats * 4;   // stem neighbour planes [8][32] u64
-constexpr int kLdsBytes = kPlanes + kS * 32 * 8;
+constexpr int kWStem = kPlanes + kS * 32 * 8;      // stem weight fragments [4 ct][64 lanes] x 16 B, staged once
+constexpr int kLdsBytes = kWStem + 4 * 64 * 16;
 constexpr int kStamps = 20;                // phase stamps per wave in the diagnostic mode (17..19: inside block 0 conv1)
 static_assert(kS * kLinK * 2 <= kHBytes, "head features fit in Y");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
@@ -115,9 +116,10 @@ __device__ __forceinline__ uint32_t pack_relu_bf16x2(float a, float b) {
 //    other orders run out of registers): wave W owns tasks [TT*W/4, TT*(W+1)/4)
 //    of task = pos_tile*CT + co_tile: ~NPT/4 position tiles, every co tile, so
 //    each wave streams all CT weight fragments per k-step;
-//  * co-major (64-channel layers, NPT <= SPAI_CO_MAJOR_MAX_NPT): wave W owns co
-//    tile W over all NPT position tiles, so the CU fetches each weight fragment
-//    once per k-step (4 KiB) at NPT LDS reads per wave;
+//  * co-major (NPT <= SPAI_CO_MAJOR_MAX_NPT): in the 64-channel layers wave W
+//    owns co tile W over all NPT position tiles, so the CU fetches each weight
+//    fragment once per k-step (4 KiB) at NPT LDS reads per wave; in the head
+//    (CT = 3) a wave's contiguous task range spans at most 2 co tiles;
 //  * pair split (64-channel layers, NPT <= SPAI_PAIR_MAX_NPT): wave (j = W>>1, h = W&1) owns co
 //    tiles {2j, 2j+1} over position tiles [h*m, h*m+m) (m = NPT/2) plus, for
 //    odd NPT, the last tile in co tile 2j+h: NPT tasks per wave, 2 weight
@@ -134,7 +136,7 @@ __device__ __forceinline__ uint32_t pack_relu_bf16x2(float a, float b) {
 #endif
 template <int W, int CT, int NPT>
 struct Plan {
-    static constexpr int MODE = CT != 4 ? 0 : NPT <= SPAI_CO_MAJOR_MAX_NPT ? 1 : NPT <= SPAI_PAIR_MAX_NPT ? 2 : 0;
+    static constexpr int MODE = NPT <= SPAI_CO_MAJOR_MAX_NPT ? 1 : CT == 4 && NPT <= SPAI_PAIR_MAX_NPT ? 2 : 0;
     static constexpr int TT = NPT * CT;
     // position-major / co-major: a contiguous task range
     static constexpr int first = TT * W / 4;
@@ -326,7 +328,7 @@ __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const fl
     const int col = lane & 15, q = lane >> 4;
     uint4 a[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) a[c] = P.w_stem[c * 64 + lane];
+    for (int c = 0; c < 4; ++c) a[c] = ((const uint4 *)(smem + kWStem))[c * 64 + lane];
     uint4 bv[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -535,6 +537,7 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
 
     if (tid < 64) ((uint32_t *)(smem + kZ))[tid] = 0u;
     else if (tid < 128) ((uint32_t *)(smem + kZ1))[tid - 64] = 0u;
+    ((uint4 *)(smem + kWStem))[tid] = P.w_stem[tid];   // 256 x 16 B
     {
         float *bias = (float *)(smem + kBias);
         const int nres = 2 * P.blocks * kHid;
