@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--cpu-games", type=int, default=256)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--rules-bench", action="store_true", help="also time the batched rules kernels")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r01", "forward_traffic.json"),
+                    help="PMC summary (scripts/gpu_traffic.sh) of this bench command: HBM bytes per k_forward launch")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -261,6 +263,15 @@ def main():
     ev = timing["evaluate"]
     achieved = fpe * ev["items"] / (ev["total_ms"] * 1e-3) / 1e12 if ev["total_ms"] > 0 else None
     per_launch_flop = fpe * ev["items"] / ev["launches"] if ev["launches"] else None
+    traffic, traffic_src = None, None
+    if os.path.exists(args.traffic_json):   # measured by separate rocprofv3 --pmc passes of this command
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        if "k_forward<false>" in tj:
+            traffic = tj["k_forward<false>"]["hbm_bytes_per_launch"]
+            traffic_src = ("%s: (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch over %d launches "
+                           "(FETCH doubled for gfx950)" % (os.path.relpath(args.traffic_json, REPO),
+                                                           tj["k_forward<false>"]["launches"]))
     result = {
         "metric": METRIC,
         "value": sims / dt_max,
@@ -284,7 +295,8 @@ def main():
         "kernel_ms": {k: v["avg_ms"] for k, v in timing.items()},
         "roofline": {"bound": "mfma", "kernel": "k_forward (fused 6x64 ResNet)",
                      "achieved": achieved, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / BF16_PEAK_TFLOPS if achieved else None, "traffic": None,
+                     "frac": achieved / BF16_PEAK_TFLOPS if achieved else None, "traffic": traffic,
+                     "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                      "flop_per_launch": per_launch_flop, "flop_per_eval": fpe,
                      "avg_launch_ms": ev["avg_ms"], "avg_leaves_per_launch": ev["items"] / max(1, ev["launches"])},
     }
