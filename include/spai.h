@@ -188,6 +188,46 @@ int spai_engine_timing_items(spai_engine *eng, double *total_ms, double *items);
  * the production library returns SPAI_ERR_UNSUPPORTED.  Never on the timed path. */
 int spai_net_phase_cycles(spai_net *net, uint32_t count, double *cycles);
 
+/* ---------------------------------------------------------------- learner
+ * The training step of the C4 net on the device:
+ * ModelTrainerWorker::train_batch (learner_concurrent.rs:72-85) = forward in
+ * train mode (BatchNorm batch statistics, running statistics with momentum
+ * 0.1), loss -(log_softmax(p)·pi).sum()/B + MSE(v, z) (model/mod.rs:128-135),
+ * backward, and one Adam step (tch Adam::default(), lr 1e-3, model/mod.rs:107).
+ * Parameters use spai_net_create's flat construction order, so
+ * spai_learner_params() feeds spai_net_create() for the self-play replicas.
+ * With a communicator (spai_learner_set_comm) the gradients are summed over
+ * ranks with RCCL and scaled by 1/world, and the BN running statistics are
+ * averaged: a data-parallel learner whose replicas stay identical. */
+typedef struct spai_learner spai_learner;
+typedef struct spai_adam_config {
+    float lr;            /* 1e-3 */
+    float beta1, beta2;  /* 0.9, 0.999 */
+    float eps;           /* 1e-8 */
+    float bn_momentum;   /* 0.1 */
+    float bn_eps;        /* 1e-5 */
+} spai_adam_config;
+#define SPAI_COMM_ID_BYTES 128
+
+int spai_adam_config_default(spai_adam_config *cfg);
+int spai_learner_create(spai_engine *eng, int blocks, int hidden, const float *params, size_t n_params,
+                        const spai_adam_config *cfg /* NULL = defaults */, spai_learner **out);
+int spai_learner_destroy(spai_learner *l);
+/* one optimizer step on n samples: states [n][3][6][7] (spai_encode layout),
+ * policies [n][7], values [n]; loss[3] = total, policy, value (may be NULL) */
+int spai_learner_train_batch(spai_learner *l, uint32_t n, const float *states, const float *policies,
+                             const float *values, float *loss);
+/* current parameters (incl. BN running statistics) / last step's gradients
+ * (after the cross-rank reduction, before the 1/world scale), flat order */
+int spai_learner_params(spai_learner *l, float *params, size_t n_params);
+int spai_learner_grads(spai_learner *l, float *grads, size_t n_params);
+/* RCCL communicator for a data-parallel learner: rank 0 makes the id
+ * (spai_comm_unique_id), the host side broadcasts it, every rank joins.
+ * world 1 with an id builds a 1-rank communicator (the all-reduce is then a
+ * copy); world 1 with NULL drops the communicator. */
+int spai_comm_unique_id(uint8_t *id /* SPAI_COMM_ID_BYTES */);
+int spai_learner_set_comm(spai_learner *l, int rank, int world, const uint8_t *id);
+
 #ifdef __cplusplus
 }
 #endif

@@ -384,3 +384,65 @@ int spai_engine_timing_items(spai_engine *e, double *total_ms, double *items) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- learner
+int spai_adam_config_default(spai_adam_config *cfg) {
+    PTR_CHECK(cfg);
+    cfg->lr = 1e-3f;   // Adam::default().build(vs, 1e-3) (model/mod.rs:107)
+    cfg->beta1 = 0.9f;
+    cfg->beta2 = 0.999f;
+    cfg->eps = 1e-8f;
+    cfg->bn_momentum = 0.1f;   // nn::batch_norm2d(.., Default::default())
+    cfg->bn_eps = 1e-5f;
+    return SPAI_OK;
+}
+
+int spai_learner_create(spai_engine *e, int blocks, int hidden, const float *params, size_t n,
+                        const spai_adam_config *cfg, spai_learner **out) {
+    ENG_CHECK(e);
+    PTR_CHECK(params);
+    PTR_CHECK(out);
+    return learner_create(e, blocks, hidden, params, n, cfg, out);
+}
+
+int spai_learner_destroy(spai_learner *l) {
+    if (!l) return SPAI_OK;
+    learner_destroy(l);
+    return SPAI_OK;
+}
+
+int spai_learner_train_batch(spai_learner *l, uint32_t n, const float *states, const float *policies,
+                             const float *values, float *loss) {
+    PTR_CHECK(l);
+    PTR_CHECK(states);
+    PTR_CHECK(policies);
+    PTR_CHECK(values);
+    ENG_CHECK(l->eng);
+    return learner_train_batch(l, n, states, policies, values, loss);
+}
+
+int spai_learner_params(spai_learner *l, float *params, size_t n) {
+    PTR_CHECK(l);
+    PTR_CHECK(params);
+    ENG_CHECK(l->eng);
+    return learner_params(l, params, n, false);
+}
+
+int spai_learner_grads(spai_learner *l, float *grads, size_t n) {
+    PTR_CHECK(l);
+    PTR_CHECK(grads);
+    ENG_CHECK(l->eng);
+    return learner_params(l, grads, n, true);
+}
+
+int spai_comm_unique_id(uint8_t *id) {
+    PTR_CHECK(id);
+    return comm_unique_id(id);
+}
+
+int spai_learner_set_comm(spai_learner *l, int rank, int world, const uint8_t *id) {
+    PTR_CHECK(l);
+    ENG_CHECK(l->eng);
+    if (world > 1) PTR_CHECK(id);   // world 1: an id makes a 1-rank RCCL communicator, NULL none
+    return learner_set_comm(l, rank, world, id);
+}

@@ -124,6 +124,33 @@ struct spai_net {
     spai::DevBuf<uint32_t> io_count;
 };
 
+// Device training step of the C4 net (learner.hip).
+struct spai_learner {
+    spai_engine *eng = nullptr;
+    int blocks = 0, hidden = 0;
+    spai_adam_config cfg{};
+    uint64_t step = 0;
+    uint32_t max_batch = 0;
+    size_t n_params = 0;
+    struct Conv {
+        int ci, co;
+        size_t w, b, g, be, mu, var;   // offsets into the flat parameter array
+    };
+    std::vector<Conv> convs;            // stem, 2*blocks residual, policy head, value head
+    size_t pol_w = 0, pol_b = 0, val_w = 0, val_b = 0;
+    spai::DevBuf<float> p, g, m, v;     // params, grads, Adam moments (flat)
+    spai::DevBuf<float> wt;             // flipped/transposed conv weights for the data gradient
+    spai::DevBuf<float> x_in, pi, zv;   // batch
+    std::vector<spai::DevBuf<float>> z, a, mean, invstd;   // per conv layer
+    spai::DevBuf<float> d0, d1, d2;     // backward scratch [B][64][42]
+    spai::DevBuf<float> dlogits, dpre, loss_terms, wpart, bpart;
+    spai::DevBuf<uint32_t> run_idx;     // BN running-stat offsets (for the cross-rank average)
+    spai::DevBuf<float> run_buf;
+    void *comm = nullptr;            // ncclComm_t (learner.hip)
+    int rank = 0, world = 1;
+};
+
+
 struct spai_engine {
     int game = SPAI_GAME_CONNECT4;
     int device = 0;
@@ -170,6 +197,16 @@ void net_init_params(int game, int blocks, int hidden, uint64_t seed, float *par
 // evaluate `count` (device scalar) leaves of the batch; grid sized for max_n
 int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint32_t max_n,
                    const uint64_t *mine, const uint64_t *theirs, float *priors, float *value);
+
+// learner.hip
+int learner_create(spai_engine *e, int blocks, int hidden, const float *params, size_t n, const spai_adam_config *cfg,
+                   spai_learner **out);
+void learner_destroy(spai_learner *l);
+int learner_train_batch(spai_learner *l, uint32_t n, const float *states, const float *policies, const float *values,
+                        float *loss3);
+int learner_params(spai_learner *l, float *params, size_t n, bool grads);
+int learner_set_comm(spai_learner *l, int rank, int world, const uint8_t *id);
+int comm_unique_id(uint8_t *id);
 
 // search.hip
 int trees_create(spai_engine *e, uint32_t n);

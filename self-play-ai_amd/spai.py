@@ -32,8 +32,11 @@ SYMBOLS = [
     "spai_net_destroy", "spai_net_forward", "spai_predict", "spai_engine_set_net", "spai_trees_create",
     "spai_tree_reset", "spai_search", "spai_tree_use_subtree", "spai_tree_node", "spai_tree_size",
     "spai_selfplay_run", "spai_engine_set_timing", "spai_engine_timing", "spai_engine_timing_items",
-    "spai_net_phase_cycles",
+    "spai_net_phase_cycles", "spai_adam_config_default", "spai_learner_create", "spai_learner_destroy",
+    "spai_learner_train_batch", "spai_learner_params", "spai_learner_grads", "spai_comm_unique_id",
+    "spai_learner_set_comm",
 ]
+COMM_ID_BYTES = 128
 
 
 class SpaiError(RuntimeError):
@@ -54,6 +57,10 @@ class Config(C.Structure):
 
 class SelfPlayStats(C.Structure):
     _fields_ = [(k, C.c_double) for k in ("sims", "evals", "games", "positions", "moves", "seconds")]
+
+
+class AdamConfig(C.Structure):
+    _fields_ = [(k, C.c_float) for k in ("lr", "beta1", "beta2", "eps", "bn_momentum", "bn_eps")]
 
 
 SINK = C.CFUNCTYPE(None, C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_float), C.POINTER(C.c_float),
@@ -109,6 +116,14 @@ def lib():
         L.spai_engine_timing.argtypes = [vp, vp, vp]
         L.spai_engine_timing_items.argtypes = [vp, vp, vp]
         L.spai_net_phase_cycles.argtypes = [vp, u32, vp]
+        L.spai_adam_config_default.argtypes = [P(AdamConfig)]
+        L.spai_learner_create.argtypes = [vp, i32, i32, vp, C.c_size_t, P(AdamConfig), P(vp)]
+        L.spai_learner_destroy.argtypes = [vp]
+        L.spai_learner_train_batch.argtypes = [vp, u32, vp, vp, vp, vp]
+        L.spai_learner_params.argtypes = [vp, vp, C.c_size_t]
+        L.spai_learner_grads.argtypes = [vp, vp, C.c_size_t]
+        L.spai_comm_unique_id.argtypes = [vp]
+        L.spai_learner_set_comm.argtypes = [vp, i32, i32, vp]
         _lib = L
     return _lib
 
@@ -340,3 +355,53 @@ class Engine:
         names = ("select", "evaluate", "expand")
         return {nm: dict(avg_ms=avg[i], launches=launches[i], total_ms=tot[i], items=items[i])
                 for i, nm in enumerate(names)}
+
+
+class Learner:
+    """Device training step (ModelTrainerWorker::train_batch, learner_concurrent.rs:72-85):
+    train-mode forward, policy NLL + value MSE, backward, one Adam step."""
+
+    def __init__(self, engine, blocks, params, hidden=64, **adam):
+        cfg = AdamConfig()
+        _check(lib().spai_adam_config_default(C.byref(cfg)))
+        for k, v in adam.items():
+            setattr(cfg, k, float(v))
+        self.params0 = np.ascontiguousarray(params, np.float32)
+        self.n = len(self.params0)
+        self.h = C.c_void_p()
+        _check(lib().spai_learner_create(engine.h, blocks, hidden, _p(self.params0), self.n, C.byref(cfg),
+                                         C.byref(self.h)))
+
+    def train_batch(self, states, policies, values):
+        x = np.ascontiguousarray(states, np.float32).reshape(-1, 126)
+        pi = np.ascontiguousarray(policies, np.float32).reshape(-1, 7)
+        z = np.ascontiguousarray(values, np.float32).reshape(-1)
+        assert len(x) == len(pi) == len(z)
+        loss = np.zeros(3, np.float32)
+        _check(lib().spai_learner_train_batch(self.h, len(x), _p(x), _p(pi), _p(z), _p(loss)))
+        return loss   # total, policy, value
+
+    def params(self):
+        out = np.zeros(self.n, np.float32)
+        _check(lib().spai_learner_params(self.h, _p(out), self.n))
+        return out
+
+    def grads(self):
+        out = np.zeros(self.n, np.float32)
+        _check(lib().spai_learner_grads(self.h, _p(out), self.n))
+        return out
+
+    def set_comm(self, rank, world, uid=None):
+        buf = None if uid is None else np.frombuffer(bytes(uid), np.uint8).copy()
+        _check(lib().spai_learner_set_comm(self.h, rank, world, None if buf is None else _p(buf)))
+
+    def close(self):
+        if self.h:
+            lib().spai_learner_destroy(self.h)
+            self.h = C.c_void_p()
+
+
+def comm_unique_id():
+    buf = np.zeros(COMM_ID_BYTES, np.uint8)
+    _check(lib().spai_comm_unique_id(_p(buf)))
+    return buf.tobytes()

@@ -23,6 +23,7 @@ Outputs (all small):
 import json
 import math
 import os
+import sys
 import random
 import struct
 
@@ -580,6 +581,102 @@ def net_golden(game, blocks, hidden, seed, n_pos, pos_seed):
                 boards=bb, meta=np.array([blocks, hidden, seed], np.int64))
 
 
+def learner_golden(blocks=1, hidden=64, seed=0, B=32, K=3, data_seed=21):
+    """ModelTrainerWorker::train_batch (learner_concurrent.rs:72-85) in PyTorch CPU
+    fp32: train-mode forward (BN batch stats, running stats momentum 0.1),
+    -(log_softmax(p)*pi).sum()/B + mse(v, z), backward, torch.optim.Adam(lr=1e-3)
+    (tch Adam::default(): betas 0.9/0.999, eps 1e-8, no weight decay)."""
+    import torch
+    import torch.nn.functional as F
+    params, dims = philox_params("c4", blocks, hidden, seed)
+    C, H, W, A = dims
+    # flat construction order -> tensors; running stats are buffers (no grad)
+    flat = torch.from_numpy(params.copy())
+    tensors, trainable, off = [], [], [0]
+
+    def take(shape, train=True):
+        n = int(np.prod(shape))
+        t = flat[off[0]:off[0] + n].clone().reshape(shape)
+        if train:
+            t.requires_grad_(True)
+            trainable.append(t)
+        tensors.append(t)
+        off[0] += n
+        return t
+
+    def conv(ci, co):
+        return dict(w=take((co, ci, 3, 3)), b=take((co,)), g=take((co,)), be=take((co,)),
+                    mu=take((co,), False), var=take((co,), False))
+
+    stem = conv(C, hidden)
+    res = [(conv(hidden, hidden), conv(hidden, hidden)) for _ in range(blocks)]
+    pconv = conv(hidden, 32)
+    plw, plb = take((A, 32 * H * W)), take((A,))
+    vconv = conv(hidden, 3)
+    vlw, vlb = take((1, 3 * H * W)), take((1,))
+    assert off[0] == len(params)
+
+    def cbn(t, c, relu=True):
+        t = F.conv2d(t, c["w"], c["b"], padding=1)
+        t = F.batch_norm(t, c["mu"], c["var"], c["g"], c["be"], training=True, momentum=0.1, eps=1e-5)
+        return F.relu(t) if relu else t
+
+    def forward(x):
+        t = cbn(x.view(-1, C, H, W), stem)
+        for c1, c2 in res:
+            t = F.relu(t + cbn(cbn(t, c1), c2, relu=False))
+        logits = F.linear(cbn(t, pconv).flatten(1), plw, plb)
+        value = torch.tanh(F.linear(cbn(t, vconv).flatten(1), vlw, vlb))
+        return logits, value
+
+    opt = torch.optim.Adam(trainable, lr=1e-3, foreach=False)
+    rng = random.Random(data_seed)
+    nprng = np.random.default_rng(data_seed)
+    xs, pis, zs = [], [], []
+    for _ in range(K):
+        st = []
+        while len(st) < B:
+            g = C4()
+            for _ in range(rng.randrange(0, 30)):
+                if g.status != ONGOING:
+                    break
+                g = g.next_state(rng.choice(g.valid()))
+            if g.status == ONGOING:
+                st.append(g)
+        xs.append(np.stack([g.encoding() for g in st]).astype(np.float32))
+        pi = nprng.random((B, A)).astype(np.float32) ** 3
+        pis.append((pi / pi.sum(1, keepdims=True)).astype(np.float32))
+        zs.append(nprng.choice(np.array([-1.0, 0.0, 1.0], np.float32), B))
+    losses, grads1, params1 = [], None, None
+
+    def flat_now(use_grad):
+        out = []
+        for t in tensors:
+            if use_grad:
+                out.append((t.grad if t.grad is not None else torch.zeros_like(t)).detach().reshape(-1))
+            else:
+                out.append(t.detach().reshape(-1))
+        return torch.cat(out).numpy().astype(np.float32)
+
+    for k in range(K):
+        x, pi, z = torch.from_numpy(xs[k]), torch.from_numpy(pis[k]), torch.from_numpy(zs[k]).view(-1, 1)
+        opt.zero_grad()
+        logits, value = forward(x)
+        lp = -(logits.log_softmax(-1) * pi).sum() / logits.shape[0]
+        lv = F.mse_loss(value, z)
+        loss = lp + lv
+        loss.backward()
+        if k == 0:
+            grads1 = flat_now(True)
+        opt.step()
+        losses.append([loss.item(), lp.item(), lv.item()])
+        if k == 0:
+            params1 = flat_now(False)
+    return dict(states=np.stack(xs), policies=np.stack(pis), values=np.stack(zs), loss=np.array(losses, np.float32),
+                grads1=grads1, params1=params1, params3=flat_now(False),
+                meta=np.array([blocks, hidden, seed, B, K], np.int64))
+
+
 def main():
     rules = {"traces": rules_traces(C4, 200, 1), "kats": c4_kats(), "games": moves_of(C4, 50, 2)}
     with open(os.path.join(HERE, "rules_c4.json"), "w") as f:
@@ -617,7 +714,16 @@ def main():
 
     np.savez_compressed(os.path.join(HERE, "net_c4_2x64.npz"), **net_golden("c4", 2, 64, 1234, 256, 5))
     np.savez_compressed(os.path.join(HERE, "net_ttt_2x64.npz"), **net_golden("ttt", 2, 64, 99, 64, 6))
+    learner_main()
+
+
+def learner_main():
+    np.savez_compressed(os.path.join(HERE, "learner_c4_1x64.npz"), **learner_golden())
 
 
 if __name__ == "__main__":
-    main()
+    # `gen_golden.py learner` regenerates only the training fixture
+    if len(sys.argv) > 1 and sys.argv[1] == "learner":
+        learner_main()
+    else:
+        main()

@@ -378,3 +378,76 @@ def _oracle_state(oracle, x, o, n, status):
     st.current_player = oracle.X if n % 2 == 0 else oracle.O
     st.status = status
     return oracle.C4(st)
+
+
+# ------------------------------------------------------------------ learner
+def test_learner_vs_torch_golden(spai):
+    """device train step (fp32) vs PyTorch CPU fp32: 3 Adam steps of a 1x64 net"""
+    from test_oracle_golden import check_learner_params
+    z = np.load(os.path.join(GOLDEN, "learner_c4_1x64.npz"))
+    blocks, hidden, seed, B, K = [int(v) for v in z["meta"]]
+    e = spai.Engine(num_searches=1, max_trees=1)
+    L = spai.Learner(e, blocks, spai.init_params(blocks, hidden, seed=seed), hidden=hidden)
+    losses = []
+    for k in range(K):
+        losses.append(L.train_batch(z["states"][k], z["policies"][k], z["values"][k]))
+        if k == 0:
+            g1, P1 = L.grads(), L.params()
+    P3 = L.params()
+    np.testing.assert_allclose(np.array(losses), z["loss"], rtol=1e-4, atol=1e-5)
+    g_ref = z["grads1"]
+    assert np.abs(g1 - g_ref).max() <= 1e-4 * np.abs(g_ref).max()
+    check_learner_params(P1, z["params1"], [g_ref], blocks, hidden, 1)
+    check_learner_params(P3, z["params3"], [g_ref], blocks, hidden, 3, tol=1e-4)
+    L.close()
+    e.close()
+
+
+@pytest.mark.parametrize("blocks,B,steps", [(2, 48, 2), (6, 128, 1), (0, 5, 1)])
+def test_learner_vs_oracle(spai, oracle, blocks, B, steps):
+    """other depths and batch sizes (incl. the reference's 128 and a tiny odd one)
+    vs the numpy float64 restatement"""
+    import learner_ref as LR
+    from test_oracle_golden import check_learner_params
+    rng = np.random.default_rng(blocks * 100 + B)
+    states = _reachable_positions(spai, 4 * B, 10, seed=B)
+    e = spai.Engine(num_searches=1, max_trees=1)
+    e.games_resize(len(states))
+    e.games_write(states)
+    x_all = e.encode(len(states)).reshape(len(states), 126)
+    batches = []
+    for k in range(steps):
+        x = x_all[k * B:(k + 1) * B]
+        pi = rng.random((B, 7)).astype(np.float32) ** 2
+        batches.append((x, (pi / pi.sum(1, keepdims=True)).astype(np.float32),
+                        rng.choice(np.array([-1, 0, 1], np.float32), B)))
+    p0 = spai.init_params(blocks, 64, seed=blocks + 7)
+    L = spai.Learner(e, blocks, p0)
+    dev_losses = [L.train_batch(*b) for b in batches[:1]]
+    g1 = L.grads()
+    dev_losses += [L.train_batch(*b) for b in batches[1:]]
+    P_ref, ref_losses, ref_grads = LR.train(p0, batches, blocks, 64)
+    np.testing.assert_allclose(np.array(dev_losses), ref_losses, rtol=1e-4, atol=1e-5)
+    assert np.abs(g1 - ref_grads[0]).max() <= 3e-4 * np.abs(ref_grads[0]).max()   # fp32 through 2*blocks+3 layers
+    check_learner_params(L.params(), P_ref, ref_grads, blocks, 64, steps, tol=1e-4)
+    L.close()
+    e.close()
+
+
+def test_learner_rccl_single_rank(spai):
+    """the RCCL path (gradient all-reduce + running-stat average) on a 1-rank
+    communicator must leave the step bit-identical to the plain step"""
+    z = np.load(os.path.join(GOLDEN, "learner_c4_1x64.npz"))
+    blocks, hidden, seed, B, K = [int(v) for v in z["meta"]]
+    out = []
+    for use_comm in (False, True):
+        e = spai.Engine(num_searches=1, max_trees=1)
+        L = spai.Learner(e, blocks, spai.init_params(blocks, hidden, seed=seed), hidden=hidden)
+        if use_comm:
+            L.set_comm(0, 1, spai.comm_unique_id())
+        loss = [L.train_batch(z["states"][k], z["policies"][k], z["values"][k]) for k in range(K)]
+        out.append((np.array(loss), L.params()))
+        L.close()
+        e.close()
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])

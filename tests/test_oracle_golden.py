@@ -196,3 +196,54 @@ def _c4_from_bitboards(oracle, x, o):
     st.num_actions_played = n
     st.current_player = oracle.X if n % 2 == 0 else oracle.O
     return oracle.C4(st)
+
+
+# ------------------------------------------------------------------ learner
+def learner_masks(blocks, hidden, g_refs, rel=3e-3):
+    """params whose Adam updates are well conditioned at every step given (|grad| above
+    rel * max|grad|, ten times the gradient tolerance of the tests, so its sign is
+    certain; far above fp32 noise and eps=1e-8) vs the rest.  Conv biases feeding a BatchNorm have a
+    mathematically zero gradient (BN removes the batch mean): in fp32 it is rounding
+    noise that Adam's g/(|g|+eps) turns into steps of up to lr, so those entries (and
+    any entry whose gradient is that small at some step) are only bounded by lr."""
+    import learner_ref as LR
+    convs, lin, n = LR._layout(blocks, hidden)
+    running = np.zeros(n, bool)
+    for c in convs:
+        running[c["mu"]:c["mu"] + c["co"]] = True
+        running[c["var"]:c["var"] + c["co"]] = True
+    well = ~running
+    for g in g_refs:
+        well &= np.abs(g) > rel * np.abs(g).max()
+    return well, running
+
+
+def check_learner_params(P, P_ref, g_refs, blocks, hidden, steps, lr=1e-3, tol=2e-5):
+    """g_refs: reference gradients of every step, or of step 1 only (then, for steps > 1,
+    the bound holds for 99.9 % of the step-1 well-conditioned entries)"""
+    well, running = learner_masks(blocks, hidden, g_refs)
+    # BN running stats: exact functions of the batch statistics at step 1; later steps
+    # inherit the pre-BN bias noise (a bias shifts the batch mean one-for-one)
+    np.testing.assert_allclose(P[running], P_ref[running], rtol=1e-4, atol=1e-5 if steps == 1 else lr * steps)
+    err = np.abs(P[well] - P_ref[well])
+    if len(g_refs) >= steps:
+        assert err.max() <= tol * steps
+    else:
+        assert np.quantile(err, 0.999) <= tol * steps
+    assert np.abs(P - P_ref).max() <= 2 * lr * steps + 1e-5                          # Adam step bound
+
+
+def test_learner_oracle_vs_torch_golden(oracle):
+    """numpy float64 train-step restatement vs PyTorch CPU fp32 (gen_golden.learner_golden)"""
+    import learner_ref as LR
+    z = np.load(os.path.join(GOLDEN, "learner_c4_1x64.npz"))
+    blocks, hidden, seed, B, K = [int(v) for v in z["meta"]]
+    p0 = oracle.init_params(oracle.GAME_CONNECT4, blocks, hidden, seed)
+    batches = [(z["states"][k], z["policies"][k], z["values"][k]) for k in range(K)]
+    P3, losses, grads = LR.train(p0, batches, blocks, hidden)
+    np.testing.assert_allclose(losses, z["loss"], rtol=1e-5, atol=1e-6)
+    g_ref = z["grads1"]
+    assert np.abs(grads[0] - g_ref).max() <= 1e-5 * np.abs(g_ref).max()
+    P1, _, _ = LR.train(p0, batches[:1], blocks, hidden)
+    check_learner_params(P1, z["params1"], [g_ref], blocks, hidden, 1)
+    check_learner_params(P3, z["params3"], [g_ref], blocks, hidden, 3, tol=1e-4)
