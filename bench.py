@@ -194,32 +194,25 @@ def run_cpu_baseline(args):
 
 # ---------------------------------------------------------------- GPU bench
 class Dist:
+    """one process per GPU; host-side barrier and scalar reductions over a socket
+    group (hostgroup.py) so no torch (and no second HIP runtime) enters the GPU process"""
+
     def __init__(self):
-        self.world = int(os.environ.get("WORLD_SIZE", "1"))
-        self.rank = int(os.environ.get("RANK", "0"))
+        from hostgroup import HostGroup
+        self.g = HostGroup()
+        self.world, self.rank = self.g.world, self.g.rank
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        self.pg = None
-        if self.world > 1:
-            import torch.distributed as dist  # gloo: timing barrier + scalar reductions only
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
-            self.pg = dist
+        if "SPAI_BENCH_DEVICE" in os.environ:   # rehearsal: every rank on one device
+            self.local = int(os.environ["SPAI_BENCH_DEVICE"])
 
     def barrier(self):
-        if self.pg:
-            self.pg.barrier()
+        self.g.barrier()
 
     def reduce(self, values, op):
-        if not self.pg:
-            return list(values)
-        import torch
-        t = torch.tensor(values, dtype=torch.float64)
-        self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX if op == "max" else self.pg.ReduceOp.SUM)
-        return t.tolist()
+        return self.g.allreduce(values, op)
 
     def close(self):
-        if self.pg:
-            self.pg.destroy_process_group()
+        self.g.close()
 
 
 def main():

@@ -1,9 +1,9 @@
 """Multi-GPU path on the CPU: games shard by id with no data-path collective.
 
 Per-game trajectories depend only on (seed, game id) and the position-wise
-evaluator, so a 2-rank run (gloo, world_size 2, each rank playing its shard of
-game ids as bench.py assigns them) must reproduce the single-process run
-exactly.  The oracle stands in for each rank's engine here (no GPU)."""
+evaluator, so a 2-rank run (world_size 2 over bench.py's host group, each rank
+playing its shard of game ids as bench.py assigns them) must reproduce the
+single-process run exactly.  The oracle stands in for each rank's engine here (no GPU)."""
 import os
 import socket
 import subprocess
@@ -36,32 +36,35 @@ def test_shard_invariance_oracle(oracle):
 WORKER = textwrap.dedent("""
     import os, sys, json
     sys.path.insert(0, {repo!r}); sys.path.insert(0, os.path.join({repo!r}, "oracle"))
-    import numpy as np, torch, torch.distributed as dist
+    sys.path.insert(0, os.path.join({repo!r}, "self-play-ai_amd"))
+    import numpy as np
     import oracle
-    dist.init_process_group("gloo")
-    r, w = dist.get_rank(), dist.get_world_size()
+    from hostgroup import HostGroup                            # bench.py's host-side group
+    g = HostGroup()
+    r, w = g.rank, g.world
     G = 4
     res = oracle.self_play(oracle.GAME_CONNECT4, G, 12, 3, eval_kind=oracle.EVAL_HASH,
                            game_id_base=r * G, max_plies=42)   # bench.py: base = (step*world + rank) * G
-    sims = torch.tensor([res["sims"]], dtype=torch.float64)
-    dist.all_reduce(sims)                                      # bench.py sums work over ranks
-    t = torch.tensor([float(r + 1)], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)                   # and takes the max time
-    vals = [None] * w
-    dist.all_gather_object(vals, (res["game"].tolist(), res["value"].tolist()))
+    g.barrier()
+    (sims,) = g.allreduce([res["sims"]], "sum")                 # bench.py sums work over ranks
+    (tmax,) = g.allreduce([float(r + 1)], "max")                # and takes the max time
+    parts = g.allgather((res["game"].tolist(), res["value"].tolist()))
+    uid = g.broadcast_bytes(bytes(range(128)) if r == 0 else None)   # the RCCL unique-id hand-off
+    assert uid == bytes(range(128))
     if r == 0:
-        print(json.dumps({{"sims": sims.item(), "tmax": t.item(), "parts": vals}}))
-    dist.destroy_process_group()
+        print(json.dumps({{"sims": sims, "tmax": tmax, "parts": parts}}))
+    g.close()
 """)
 
 
-def test_two_rank_gloo(oracle, tmp_path):
+def test_two_rank_host_group(oracle, tmp_path):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     script = tmp_path / "worker.py"
     script.write_text(WORKER.format(repo=REPO))
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SPAI_GROUP_PORT=str(port),
+               WORLD_SIZE="2")
     procs = [subprocess.Popen([sys.executable, str(script)], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
     outs = [p.communicate(timeout=240) for p in procs]
