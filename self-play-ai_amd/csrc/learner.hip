@@ -12,10 +12,9 @@
 // Adam, and the BN running statistics are averaged, so every rank holds the
 // same parameters after every step.
 //
-// Layout: fp32 NCHW activations [B][C][42] (the training batch is small —
-// 128 in the reference — and the step is ~15 GFLOP, far from any roofline
-// that matters next to self-play; kernels are LDS-tiled fp32 and
-// deterministic: every reduction has a fixed order, no float atomics).
+// Layout: fp32 NCHW activations [B][C][42].  The convs (forward, data and
+// weight gradients) run on the exact-f32 MFMA; every reduction has a fixed
+// order and there are no float atomics, so a step is deterministic.
 // Parameters, gradients and Adam moments share the flat construction-order
 // layout of spai_net_create (conv w, b, BN γ, β, μ, σ²; linears w, b).
 #include <rccl/rccl.h>
@@ -32,108 +31,252 @@ namespace {
 
 constexpr int kCells = 42, kRows = 6, kCols = 7;
 constexpr int kPad = 72;          // (6+2) x (7+2) zero-padded plane
+constexpr int kPlane = 73;        // its LDS stride (odd, so channels spread over the banks)
 constexpr int kThreads = 256;
-constexpr int kWgradSplit = 8;    // batch chunks of the weight-gradient reduction
 
-// ------------------------------------------------------------------ conv 3x3
-// out[b][co][p] (+)= bias[co] + sum_ci sum_tap w[co][ci][tap] * in[b][ci][p + off(tap)]
-// One workgroup per (sample, block of up to 16 output channels): the sample's
-// zero-padded input planes and the block's weights are staged in LDS.
-// Also the data gradient: dx = conv(dz, w') with w'[ci][co][8 - tap].
-__global__ __launch_bounds__(kThreads) void k_conv3x3(const float *__restrict__ in, int ci_n,
-                                                      const float *__restrict__ w, const float *__restrict__ bias,
-                                                      int co_n, int cob, float *__restrict__ out, int accumulate) {
-    extern __shared__ float sm[];
-    float *xs = sm;                      // [ci_n][kPad]
-    float *ws = sm + ci_n * kPad;        // [cob][ci_n][9]
-    const int b = blockIdx.y, co0 = blockIdx.x * cob;
-    const int ncob = min(cob, co_n - co0);
-    const float *xb = in + (size_t)b * ci_n * kCells;
-    for (int i = threadIdx.x; i < ci_n * kPad; i += kThreads) {
+// ------------------------------------------------------------------ conv 3x3 on f32 MFMA
+// Every conv of the step is a GEMM on v_mfma_f32_16x16x4_f32 (exact f32: an
+// fmaf chain per output element; 157 TF/s peak, the f32 vector rate).  The
+// reduction index is tap-major, k = tap * cinp + c (cinp = input channels
+// rounded up to 4), so one k-step of 4 stays inside one tap and a lane's LDS
+// address is its position's tap offset plus the channel.
+//   forward:  out[b][n][p] = bias[n] + sum_k X[b][p][k] * Wk[k][n]
+//   data grad: the same with X = dz and Wk built from the flipped, transposed
+//              weights (w'[ci][co][8 - tap] = w[co][ci][tap])
+//   weight grad: part[b][n][k] = sum_p dz[b][n][p] * X[b][p][k], then a
+//              fixed-order sum over the batch (deterministic, no atomics)
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__host__ __device__ inline int round4(int c) { return (c + 3) & ~3; }
+__host__ __device__ inline int round16(int c) { return (c + 15) & ~15; }
+
+// tap offset inside a zero-padded 8 x 9 plane
+__device__ __forceinline__ int tap_off(int tap) { return (tap / 3 - 1) * 9 + (tap % 3 - 1); }
+
+// stage a sample's input planes [c][kPlane], zero-padded (rows -1..6, cols -1..7), channels >= cin zero.
+// All of a thread's loads are issued before its LDS stores, so the staging pays
+// one memory round trip, not one per element.
+constexpr int kStageMax = (64 * kPad + kThreads - 1) / kThreads;   // 18 elements per thread at 64 channels
+__device__ __forceinline__ void stage_planes(const float *__restrict__ xb, int cin, int cinp, float *xs) {
+    float v[kStageMax];
+    const int n = cinp * kPad;
+#pragma unroll
+    for (int j = 0; j < kStageMax; ++j) {
+        const int i = threadIdx.x + j * kThreads;
         const int c = i / kPad, r = i - c * kPad, h = r / 9 - 1, x = r % 9 - 1;
-        xs[i] = (h >= 0 && h < kRows && x >= 0 && x < kCols) ? xb[c * kCells + h * kCols + x] : 0.f;
+        v[j] = (i < n && c < cin && h >= 0 && h < kRows && x >= 0 && x < kCols) ? xb[c * kCells + h * kCols + x] : 0.f;
     }
-    for (int i = threadIdx.x; i < ncob * ci_n * 9; i += kThreads) ws[i] = w[(size_t)co0 * ci_n * 9 + i];
-    __syncthreads();
-    for (int o = threadIdx.x; o < ncob * kCells; o += kThreads) {
-        const int co = o / kCells, p = o - co * kCells, h = p / kCols, x = p - h * kCols;
-        const float *wr = ws + co * ci_n * 9;
-        float acc = 0.f;
-        for (int c = 0; c < ci_n; ++c) {
-            const float *xp = xs + c * kPad + h * 9 + x;   // top-left of the 3x3 window
-            const float *wc = wr + c * 9;
 #pragma unroll
-            for (int t = 0; t < 9; ++t) acc += wc[t] * xp[(t / 3) * 9 + t % 3];
-        }
-        if (bias) acc += bias[co0 + co];
-        float *dst = out + ((size_t)b * co_n + co0 + co) * kCells + p;
-        *dst = accumulate ? *dst + acc : acc;
+    for (int j = 0; j < kStageMax; ++j) {
+        const int i = threadIdx.x + j * kThreads;
+        if (i < n) xs[(i / kPad) * kPlane + i % kPad] = v[j];
     }
 }
 
-// w'[ci][co][8 - tap] = w[co][ci][tap] (data-gradient weights)
-__global__ void k_flip_transpose(const float *__restrict__ w, int co_n, int ci_n, float *__restrict__ wt) {
+// Wk[(tap * cinp + c) * coutp + n]: forward Wk = w[n][c][tap]; data gradient Wk = w[c][n][8 - tap]
+__global__ void k_pack_wk(const float *__restrict__ w, int cin, int cout, int cinp, int coutp, int dgrad,
+                          float *__restrict__ wk) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= co_n * ci_n * 9) return;
-    const int co = i / (ci_n * 9), r = i - co * ci_n * 9, c = r / 9, t = r % 9;
-    wt[((size_t)c * co_n + co) * 9 + (8 - t)] = w[i];
+    if (i >= 9 * cinp * coutp) return;
+    const int n = i % coutp, k = i / coutp, tap = k / cinp, c = k - tap * cinp;
+    float v = 0.f;
+    if (c < cin && n < cout)
+        v = dgrad ? w[((size_t)c * cout + n) * 9 + (8 - tap)] : w[((size_t)n * cin + c) * 9 + tap];
+    wk[i] = v;
 }
 
-// partial weight/bias gradients over batch chunk blockIdx.y:
-// part[y][co][ci*9+tap] = sum_{b in chunk} sum_p dz[b][co][p] * x[b][ci][p + off(tap)]
-// partb[y][co] = sum_{b in chunk} sum_p dz[b][co][p]
-__global__ __launch_bounds__(kThreads) void k_conv_wgrad_part(const float *__restrict__ x, int ci_n,
-                                                              const float *__restrict__ dz, int co_n, int B,
-                                                              float *__restrict__ part, float *__restrict__ partb) {
+// one workgroup per sample: 3 position tiles (48 rows, 42 real) x NT = coutp/16
+// channel tiles; wave w owns channel tile w % NT and K part w / NT (KS = 4/NT
+// parts, summed in LDS in a fixed order).  CINP (input channels padded to 4) and
+// NT are compile-time, so the k-loop unrolls fully and the weight loads of a
+// whole part are in flight together.
+template <int CINP, int NT>
+__global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict__ in, int cin,
+                                                        const float *__restrict__ wk, const float *__restrict__ bias,
+                                                        int cout, float *__restrict__ out, int accumulate) {
+    constexpr int KS = 4 / NT, COUTP = 16 * NT, CSN = CINP / 4, KSTEPS = 9 * CSN, PER = KSTEPS / KS;
+    static_assert(KSTEPS % KS == 0, "K parts must be whole k-steps");
     extern __shared__ float sm[];
-    float *xs = sm;                 // [ci_n][kPad]
-    float *ds = sm + ci_n * kPad;   // [kCells]
-    const int co = blockIdx.x, y = blockIdx.y;
-    const int b0 = (int)((int64_t)B * y / gridDim.y), b1 = (int)((int64_t)B * (y + 1) / gridDim.y);
-    const int nout = ci_n * 9;
-    float acc[3] = {0.f, 0.f, 0.f};   // outputs tid, tid+256, tid+512 (nout <= 576)
-    float accb = 0.f;
-    for (int b = b0; b < b1; ++b) {
-        const float *xb = x + (size_t)b * ci_n * kCells;
-        for (int i = threadIdx.x; i < ci_n * kPad; i += kThreads) {
-            const int c = i / kPad, r = i - c * kPad, h = r / 9 - 1, xx = r % 9 - 1;
-            xs[i] = (h >= 0 && h < kRows && xx >= 0 && xx < kCols) ? xb[c * kCells + h * kCols + xx] : 0.f;
-        }
-        if (threadIdx.x < kCells) ds[threadIdx.x] = dz[((size_t)b * co_n + co) * kCells + threadIdx.x];
-        __syncthreads();
+    float *xs = sm;                          // [CINP][kPlane]
+    float *red = sm + CINP * kPlane;         // K-split partials [3 parts][3 mt][64 lanes][4] per channel tile
+    const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    stage_planes(in + (size_t)b * cin * kCells, cin, CINP, xs);
+    __syncthreads();
+    const int nt = wave % NT, part = wave / NT;
+    if (part >= KS) return;   // NT = 3 would leave a wave without a part (no barrier follows)
+    const int s0 = part * PER;
+    const int row = lane & 15, kq = lane >> 4;
+    int pbase[3];
+    bool pval[3];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int o = threadIdx.x + k * kThreads;
-            if (o < nout) {
-                const int c = o / 9, t = o - c * 9;
-                const float *xp = xs + c * kPad + (t / 3) * 9 + t % 3;
-                float s = 0.f;
-                for (int p = 0; p < kCells; ++p) s += ds[p] * xp[(p / kCols) * 9 + p % kCols];
-                acc[k] += s;
+    for (int mt = 0; mt < 3; ++mt) {
+        const int p = mt * 16 + row;
+        pval[mt] = p < kCells;
+        const int pp = pval[mt] ? p : 0;
+        pbase[mt] = (pp / kCols + 1) * 9 + pp % kCols + 1;
+    }
+    f32x4 acc[3] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    const float *wl = wk + (size_t)(4 * s0 + kq) * COUTP + nt * 16 + row;
+    float bq[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) bq[i] = wl[(size_t)i * 4 * COUTP];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const int s = s0 + i, tap = s / CSN, cs = s % CSN;   // CSN is a power of two here: shifts
+        const float *xc = xs + (4 * cs + kq) * kPlane + tap_off(tap);
+#pragma unroll
+        for (int mt = 0; mt < 3; ++mt) {
+            const float av = pval[mt] ? xc[pbase[mt]] : 0.f;
+            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bq[i], acc[mt], 0, 0, 0);
+        }
+    }
+    if (KS > 1) {   // fixed-order sum of the K parts
+        if (part > 0) {
+            float *dst = red + (((part - 1) * 3) * 64 + lane) * 4 + nt * (3 * 3 * 64 * 4);
+#pragma unroll
+            for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) dst[mt * 64 * 4 + r] = acc[mt][r];
+        }
+        __syncthreads();
+        if (part > 0) return;
+#pragma unroll
+        for (int q = 1; q < KS; ++q) {
+            const float *src = red + (((q - 1) * 3) * 64 + lane) * 4 + nt * (3 * 3 * 64 * 4);
+#pragma unroll
+            for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[mt][r] += src[mt * 64 * 4 + r];
+        }
+    }
+    const int n = nt * 16 + row;   // D[row = 4 kq + r][col = lane & 15]: col = channel, row = position
+    if (n >= cout) return;
+    const float bn = bias ? bias[n] : 0.f;
+    float *ob = out + ((size_t)b * cout + n) * kCells;
+#pragma unroll
+    for (int mt = 0; mt < 3; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int p = mt * 16 + 4 * kq + r;
+            if (p < kCells) {
+                const float v = acc[mt][r] + bn;
+                ob[p] = accumulate ? ob[p] + v : v;
             }
         }
-        if (threadIdx.x == 0) {
-            float s = 0.f;
-            for (int p = 0; p < kCells; ++p) s += ds[p];
-            accb += s;
-        }
-        __syncthreads();
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const int o = threadIdx.x + k * kThreads;
-        if (o < nout) part[((size_t)y * co_n + co) * nout + o] = acc[k];
-    }
-    if (threadIdx.x == 0) partb[(size_t)y * co_n + co] = accb;
 }
 
-// g[i] = sum_y part[y][i] in fixed order (deterministic)
-__global__ void k_sum_parts(const float *__restrict__ part, int n, int ny, float *__restrict__ g) {
+// weight-gradient partial of one sample: part[b][n][k] (k tap-major over cinp), and
+// partb[b][n] = sum_p dz[b][n][p].  GEMM rows = output channels (coutp/16 tiles),
+// columns = k (round16(9 cinp)/16 tiles), reduction = the 42 positions (11 k-steps of 4)
+__global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict__ x, int cin,
+                                                         const float *__restrict__ dz, int cout,
+                                                         float *__restrict__ part, float *__restrict__ partb) {
+    extern __shared__ float sm[];
+    const int cinp = round4(cin), coutp = round16(cout), K = 9 * cinp, Kp = round16(K);
+    float *xs = sm;                        // [cinp][kPlane]
+    float *ds = sm + cinp * kPlane;        // [coutp][44], zero past 42 and past cout
+    const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    stage_planes(x + (size_t)b * cin * kCells, cin, cinp, xs);
+    {   // dz rows [n][44], loads first (one round trip)
+        constexpr int M = (64 * 44 + kThreads - 1) / kThreads;
+        float v[M];
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            const int i = threadIdx.x + j * kThreads, n = i / 44, p = i - n * 44;
+            v[j] = (i < coutp * 44 && n < cout && p < kCells) ? dz[((size_t)b * cout + n) * kCells + p] : 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < M; ++j) {
+            const int i = threadIdx.x + j * kThreads;
+            if (i < coutp * 44) ds[i] = v[j];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < cout) {   // bias partial (fixed order)
+        float t = 0.f;
+        for (int p = 0; p < kCells; ++p) t += ds[threadIdx.x * 44 + p];
+        partb[(size_t)b * cout + threadIdx.x] = t;
+    }
+    const int row = lane & 15, kq = lane >> 4;
+    const int NTo = coutp / 16, NK = Kp / 16, ntiles = NTo * NK;
+    // per lane, the im2col position offsets of the 11 k-steps (p = 4 s + kq)
+    int pb[11];
+    bool pv[11];
+#pragma unroll
+    for (int s = 0; s < 11; ++s) {
+        const int p = 4 * s + kq;
+        pv[s] = p < kCells;
+        const int pp = pv[s] ? p : 0;
+        pb[s] = (pp / kCols + 1) * 9 + pp % kCols + 1;
+    }
+    constexpr int G = 4;   // tiles in flight per wave (independent MFMA chains)
+    for (int t0 = wave * G; t0 < ntiles; t0 += 4 * G) {
+        f32x4 acc[G];
+        int cols[G];        // plane base + tap offset (may be negative: c = 0, tap above/left)
+        bool kval[G];       // k < K (past K: the padded tail of the last k tile)
+        const float *arow[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+            const int t = min(t0 + g, ntiles - 1);
+            const int mt = t / NK, kt = t - mt * NK;
+            arow[g] = ds + (mt * 16 + row) * 44;           // A[m = channel][kk = position]
+            const int k = kt * 16 + row;                   // B[kk = position][n = k]
+            const int tap = k / cinp, c = k - tap * cinp;
+            kval[g] = k < K;
+            cols[g] = kval[g] ? c * kPlane + tap_off(tap) : 0;
+        }
+#pragma unroll
+        for (int s = 0; s < 11; ++s) {
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const float av = arow[g][4 * s + kq];
+                const float bv = (kval[g] && pv[s]) ? xs[cols[g] + pb[s]] : 0.f;
+                acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[g], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int t = t0 + g;
+            if (t >= ntiles) break;
+            const int mt = t / NK, kt = t - mt * NK;
+            const int k = kt * 16 + row;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int n = mt * 16 + 4 * kq + r;
+                if (n < cout && k < K) part[((size_t)b * cout + n) * K + k] = acc[g][r];
+            }
+        }
+    }
+}
+
+// dW[n][c][tap] = sum_b part[b][n][tap * cinp + c];  db[n] = sum_b partb[b][n]  (fixed order)
+__global__ void k_wgrad_reduce(const float *__restrict__ part, const float *__restrict__ partb, int B, int cin,
+                               int cout, float *__restrict__ dw, float *__restrict__ db) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    float s = 0.f;
-    for (int y = 0; y < ny; ++y) s += part[(size_t)y * n + i];
-    g[i] = s;
+    const int cinp = round4(cin), K = 9 * cinp;
+    if (i < cout * K) {   // i = n * K + k: consecutive threads read consecutive partials (coalesced)
+        const int n = i / K, k = i - n * K, tap = k / cinp, c = k - tap * cinp;
+        if (c < cin) {
+            const float *src = part + i;
+            const size_t stride = (size_t)cout * K;
+            float s = 0.f;
+            for (int b0 = 0; b0 < B; b0 += 16) {   // 16 loads in flight, summed in batch order
+                float v[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) v[j] = b0 + j < B ? src[(size_t)(b0 + j) * stride] : 0.f;
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (b0 + j < B) s += v[j];
+            }
+            dw[((size_t)n * cin + c) * 9 + tap] = s;
+        }
+    }
+    if (i < cout) {
+        float s = 0.f;
+        for (int b = 0; b < B; ++b) s += partb[(size_t)b * cout + i];
+        db[i] = s;
+    }
 }
 
 // ------------------------------------------------------------------ batch norm
@@ -344,32 +487,61 @@ int learner_alloc_batch(spai_learner *L, uint32_t B) {
     SPAI_TRY(L->dlogits.alloc((size_t)B * 7));
     SPAI_TRY(L->dpre.alloc(B));
     SPAI_TRY(L->loss_terms.alloc((size_t)B * 2));
+    const size_t cmax = (size_t)std::max(L->hidden, 32);
+    SPAI_TRY(L->wpart.alloc((size_t)B * cmax * 9 * round4(L->hidden)));   // per-sample weight-gradient partials
+    SPAI_TRY(L->bpart.alloc((size_t)B * cmax));
     L->max_batch = B;
     return SPAI_OK;
 }
 
-void launch_conv(const float *in, int ci, const float *w, const float *bias, int co, float *out, int B, bool acc,
-                 hipStream_t st) {
-    const int cob = std::min(16, co);
-    const size_t lds = ((size_t)ci * kPad + (size_t)cob * ci * 9) * sizeof(float);
-    k_conv3x3<<<dim3((co + cob - 1) / cob, B), kThreads, lds, st>>>(in, ci, w, bias, co, cob, out, acc ? 1 : 0);
+// out (+)= conv(in) on f32 MFMA; dgrad: flipped/transposed weights, no bias.
+// The learner's shapes: input channels 3 (-> 4), 32 or 64; output 3 (1 tile), 32 (2) or 64 (4).
+template <int CINP>
+int launch_conv_t(int nt, dim3 grid, size_t lds, hipStream_t st, const float *in, int cin, const float *wk,
+                  const float *bias, int cout, float *out, int acc) {
+    constexpr int ks = 9 * CINP / 4;   // k-steps; a K split into 4/NT parts needs whole k-steps per part
+    if constexpr (ks % 4 == 0) {
+        if (nt == 1) {
+            k_conv_mfma<CINP, 1><<<grid, kThreads, lds, st>>>(in, cin, wk, bias, cout, out, acc);
+            return SPAI_OK;
+        }
+    }
+    if constexpr (ks % 2 == 0) {
+        if (nt == 2) {
+            k_conv_mfma<CINP, 2><<<grid, kThreads, lds, st>>>(in, cin, wk, bias, cout, out, acc);
+            return SPAI_OK;
+        }
+    }
+    if (nt == 4) {
+        k_conv_mfma<CINP, 4><<<grid, kThreads, lds, st>>>(in, cin, wk, bias, cout, out, acc);
+        return SPAI_OK;
+    }
+    set_error("learner conv: %d input / %d output channels not built", cin, cout);
+    return SPAI_ERR_UNSUPPORTED;
 }
 
-// dW, db of one conv: split-batch partials, then a fixed-order sum
-void launch_wgrad(spai_learner *L, const float *x, int ci, const float *dz, int co, int B, float *dw, float *db,
-                  hipStream_t st) {
-    const size_t lds = ((size_t)ci * kPad + kCells) * sizeof(float);
-    const int ny = std::min(kWgradSplit, B);
-    k_conv_wgrad_part<<<dim3(co, ny), kThreads, lds, st>>>(x, ci, dz, co, B, L->wpart.p, L->bpart.p);
-    k_sum_parts<<<blocks_of((size_t)co * ci * 9), kThreads, 0, st>>>(L->wpart.p, co * ci * 9, ny, dw);
-    k_sum_parts<<<blocks_of(co), kThreads, 0, st>>>(L->bpart.p, co, ny, db);
+int launch_conv(spai_learner *L, const float *in, int cin, const float *w, const float *bias, int cout, float *out,
+                int B, bool acc, bool dgrad, hipStream_t st) {
+    const int cinp = round4(cin), coutp = round16(cout);
+    k_pack_wk<<<blocks_of((size_t)9 * cinp * coutp), kThreads, 0, st>>>(w, cin, cout, cinp, coutp, dgrad ? 1 : 0,
+                                                                        L->wt.p);
+    const size_t lds = ((size_t)cinp * kPlane + 2 * 2304) * sizeof(float);
+    const int nt = coutp / 16, a = acc ? 1 : 0;
+    switch (cinp) {
+    case 4: return launch_conv_t<4>(nt, dim3(B), lds, st, in, cin, L->wt.p, bias, cout, out, a);
+    case 32: return launch_conv_t<32>(nt, dim3(B), lds, st, in, cin, L->wt.p, bias, cout, out, a);
+    case 64: return launch_conv_t<64>(nt, dim3(B), lds, st, in, cin, L->wt.p, bias, cout, out, a);
+    default: set_error("learner conv: %d input channels not built", cin); return SPAI_ERR_UNSUPPORTED;
+    }
 }
 
-// data gradient of one conv: dx (+)= conv(dz, flip-transposed w)
-void launch_dgrad(spai_learner *L, const float *dz, int co, const float *w, int ci, float *dx, int B, bool acc,
+// dW, db of one conv: per-sample partials on f32 MFMA, then a fixed-order sum over the batch
+void launch_wgrad(spai_learner *L, const float *x, int cin, const float *dz, int cout, int B, float *dw, float *db,
                   hipStream_t st) {
-    k_flip_transpose<<<blocks_of((size_t)co * ci * 9), kThreads, 0, st>>>(w, co, ci, L->wt.p);
-    launch_conv(dz, co, L->wt.p, nullptr, ci, dx, B, acc, st);
+    const size_t lds = ((size_t)round4(cin) * kPlane + (size_t)round16(cout) * 44) * sizeof(float);
+    k_wgrad_mfma<<<B, kThreads, lds, st>>>(x, cin, dz, cout, L->wpart.p, L->bpart.p);
+    k_wgrad_reduce<<<blocks_of((size_t)cout * 9 * round4(cin)), kThreads, 0, st>>>(L->wpart.p, L->bpart.p, B, cin, cout, dw,
+                                                                          db);
 }
 
 }  // namespace
@@ -377,7 +549,7 @@ void launch_dgrad(spai_learner *L, const float *dz, int co, const float *w, int 
 int learner_create(spai_engine *e, int blocks, int hidden, const float *params, size_t n, const spai_adam_config *cfg,
                    spai_learner **out) {
     SPAI_CHECK(e->game == SPAI_GAME_CONNECT4, SPAI_ERR_UNSUPPORTED, "learner: only Connect4 is built");
-    SPAI_CHECK(hidden >= 1 && hidden <= 64, SPAI_ERR_UNSUPPORTED, "learner: hidden 1..64 (got %d)", hidden);
+    SPAI_CHECK(hidden == 64, SPAI_ERR_UNSUPPORTED, "learner: hidden must be 64 (got %d)", hidden);
     SPAI_CHECK(blocks >= 0 && blocks <= 40, SPAI_ERR_UNSUPPORTED, "learner: 0..40 blocks (got %d)", blocks);
     SPAI_CHECK(params && n == net_num_params(e->game, blocks, hidden), SPAI_ERR_INVALID, "expected %zu params, got %zu",
                net_num_params(e->game, blocks, hidden), n);
@@ -422,10 +594,7 @@ int learner_create(spai_engine *e, int blocks, int hidden, const float *params, 
     chk(L->g.alloc(n));
     chk(L->m.alloc(n));
     chk(L->v.alloc(n));
-    const size_t cmax = (size_t)std::max(hidden, 32);
-    chk(L->wt.alloc(cmax * hidden * 9));
-    chk(L->wpart.alloc((size_t)kWgradSplit * cmax * hidden * 9));
-    chk(L->bpart.alloc((size_t)kWgradSplit * cmax));
+    chk(L->wt.alloc((size_t)9 * 64 * 64));   // packed [k][n] conv weights (cin, cout <= 64)
     L->z.resize(L->convs.size());
     L->a.resize(L->convs.size());
     L->mean.resize(L->convs.size());
@@ -486,9 +655,10 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
     const int pol = (int)nl - 2, val = (int)nl - 1;
 
     // ---------------- forward (train mode)
+    int crc = SPAI_OK;   // conv launch status (shape dispatch)
     auto conv_bn_act = [&](int l, const float *in, const float *res) {
         const spai_learner::Conv &c = L->convs[l];
-        launch_conv(in, c.ci, P + c.w, P + c.b, c.co, L->z[l].p, (int)B, false, st);
+        if (crc == SPAI_OK) crc = launch_conv(L, in, c.ci, P + c.w, P + c.b, c.co, L->z[l].p, (int)B, false, false, st);
         k_bn_stats<<<c.co, kThreads, 0, st>>>(L->z[l].p, c.co, (int)B, eps, mom, L->mean[l].p, L->invstd[l].p, P + c.mu,
                                               P + c.var);
         k_bn_act<<<blocks_of((size_t)B * c.co * kCells), kThreads, 0, st>>>(L->z[l].p, c.co, (int)B, L->mean[l].p,
@@ -520,7 +690,7 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
         k_bn_bwd<<<c.co, kThreads, 0, st>>>(da, L->a[l].p, L->z[l].p, c.co, (int)B, L->mean[l].p, L->invstd[l].p,
                                             P + c.g, G + c.g, G + c.be, L->d2.p);
         launch_wgrad(L, in, c.ci, L->d2.p, c.co, (int)B, G + c.w, G + c.b, st);
-        if (dx) launch_dgrad(L, L->d2.p, c.co, P + c.w, c.ci, dx, (int)B, acc, st);
+        if (dx && crc == SPAI_OK) crc = launch_conv(L, L->d2.p, c.co, P + c.w, nullptr, c.ci, dx, (int)B, acc, true, st);
     };
     bn_conv_bwd(pol, L->d1.p, h, L->d0.p, false);
     k_linear_bwd_w<<<blocks_of(3 * kCells), kThreads, 0, st>>>(L->a[val].p, L->dpre.p, (int)B, 1, 3 * kCells,
@@ -541,7 +711,7 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
             k_bn_bwd<<<c.co, kThreads, 0, st>>>(L->d1.p, L->a[l2].p, L->z[l2].p, c.co, (int)B, L->mean[l2].p,
                                                 L->invstd[l2].p, P + c.g, G + c.g, G + c.be, L->d2.p);
             launch_wgrad(L, L->a[l1].p, c.ci, L->d2.p, c.co, (int)B, G + c.w, G + c.b, st);
-            launch_dgrad(L, L->d2.p, c.co, P + c.w, c.ci, L->d0.p, (int)B, false, st);
+            if (crc == SPAI_OK) crc = launch_conv(L, L->d2.p, c.co, P + c.w, nullptr, c.ci, L->d0.p, (int)B, false, true, st);
         }
         // BN1/conv1 backward: da = d0 (gradient wrt relu1 output), mask a[l1]; its input is hin;
         // dgrad accumulates into d1 (= dt, the skip gradient) -> d(block input)
@@ -551,6 +721,7 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
     // stem: no data gradient
     bn_conv_bwd(0, L->d0.p, L->x_in.p, nullptr, false);
 
+    SPAI_TRY(crc);
     // ---------------- cross-rank reduction + Adam
     float gscale = 1.0f;
     if (L->comm) {   // (a 1-rank communicator reduces to a copy)
