@@ -57,6 +57,38 @@ __device__ __forceinline__ int tap_off(int tap) { return (tap / 3 - 1) * 9 + (ta
 // All of a thread's loads are issued before its LDS stores, so the staging pays
 // one memory round trip, not one per element.
 constexpr int kStageMax = (64 * kPad + kThreads - 1) / kThreads;   // 18 elements per thread at 64 channels
+__device__ __forceinline__ void load_planes(const float *__restrict__ xb, int cin, int cinp, float (&v)[kStageMax]) {
+    const int n = cinp * kPad;
+#pragma unroll
+    for (int j = 0; j < kStageMax; ++j) {
+        const int i = threadIdx.x + j * kThreads;
+        const int c = i / kPad, r = i - c * kPad, h = r / 9 - 1, x = r % 9 - 1;
+        v[j] = (i < n && c < cin && h >= 0 && h < kRows && x >= 0 && x < kCols) ? xb[c * kCells + h * kCols + x] : 0.f;
+    }
+}
+__device__ __forceinline__ void store_planes(const float (&v)[kStageMax], int cinp, float *xs) {
+    const int n = cinp * kPad;
+#pragma unroll
+    for (int j = 0; j < kStageMax; ++j) {
+        const int i = threadIdx.x + j * kThreads;
+        if (i < n) xs[(i / kPad) * kPlane + i % kPad] = v[j];
+    }
+}
+constexpr int kDzMax = (64 * 44 + kThreads - 1) / kThreads;
+__device__ __forceinline__ void load_dz(const float *__restrict__ dzb, int cout, int coutp, float (&v)[kDzMax]) {
+#pragma unroll
+    for (int j = 0; j < kDzMax; ++j) {
+        const int i = threadIdx.x + j * kThreads, n = i / 44, p = i - n * 44;
+        v[j] = (i < coutp * 44 && n < cout && p < kCells) ? dzb[n * kCells + p] : 0.f;
+    }
+}
+__device__ __forceinline__ void store_dz(const float (&v)[kDzMax], int coutp, float *ds) {
+#pragma unroll
+    for (int j = 0; j < kDzMax; ++j) {
+        const int i = threadIdx.x + j * kThreads;
+        if (i < coutp * 44) ds[i] = v[j];
+    }
+}
 __device__ __forceinline__ void stage_planes(const float *__restrict__ xb, int cin, int cinp, float *xs) {
     float v[kStageMax];
     const int n = cinp * kPad;
@@ -165,41 +197,27 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
         }
 }
 
-// weight-gradient partial of one sample: part[b][n][k] (k tap-major over cinp), and
-// partb[b][n] = sum_p dz[b][n][p].  GEMM rows = output channels (coutp/16 tiles),
-// columns = k (round16(9 cinp)/16 tiles), reduction = the 42 positions (11 k-steps of 4)
+// weight-gradient partials: workgroup (chunk, group) accumulates, over the
+// kWgSamples samples of its chunk, the output tiles of its tile group:
+//   part[chunk][n][k] = sum_{b in chunk} sum_p dz[b][n][p] * X[b][p][k]   (k tap-major over CINP)
+//   partb[chunk][n]   = sum_{b in chunk} sum_p dz[b][n][p]
+// GEMM rows = output channels (coutp/16 tiles), columns = k (round16(9 CINP)/16
+// tiles), reduction = each sample's 42 positions (11 k-steps of 4).
+constexpr int kWgSamples = 4;
+constexpr int kWgMaxTiles = 9;   // tiles per wave (144 tiles / 4 groups / 4 waves at 64 x 64)
+template <int CINP>
 __global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict__ x, int cin,
-                                                         const float *__restrict__ dz, int cout,
+                                                         const float *__restrict__ dz, int cout, int B, int groups,
                                                          float *__restrict__ part, float *__restrict__ partb) {
+    constexpr int K = 9 * CINP, Kp = (K + 15) & ~15, NK = Kp / 16;
     extern __shared__ float sm[];
-    const int cinp = round4(cin), coutp = round16(cout), K = 9 * cinp, Kp = round16(K);
-    float *xs = sm;                        // [cinp][kPlane]
-    float *ds = sm + cinp * kPlane;        // [coutp][44], zero past 42 and past cout
-    const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    stage_planes(x + (size_t)b * cin * kCells, cin, cinp, xs);
-    {   // dz rows [n][44], loads first (one round trip)
-        constexpr int M = (64 * 44 + kThreads - 1) / kThreads;
-        float v[M];
-#pragma unroll
-        for (int j = 0; j < M; ++j) {
-            const int i = threadIdx.x + j * kThreads, n = i / 44, p = i - n * 44;
-            v[j] = (i < coutp * 44 && n < cout && p < kCells) ? dz[((size_t)b * cout + n) * kCells + p] : 0.f;
-        }
-#pragma unroll
-        for (int j = 0; j < M; ++j) {
-            const int i = threadIdx.x + j * kThreads;
-            if (i < coutp * 44) ds[i] = v[j];
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < cout) {   // bias partial (fixed order)
-        float t = 0.f;
-        for (int p = 0; p < kCells; ++p) t += ds[threadIdx.x * 44 + p];
-        partb[(size_t)b * cout + threadIdx.x] = t;
-    }
+    const int coutp = round16(cout), NTo = coutp / 16, ntiles = NTo * NK;
+    float *xs = sm;                        // [CINP][kPlane]
+    float *ds = sm + CINP * kPlane;        // [coutp][44], zero past 42 and past cout
+    const int chunk = blockIdx.x, group = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int row = lane & 15, kq = lane >> 4;
-    const int NTo = coutp / 16, NK = Kp / 16, ntiles = NTo * NK;
-    // per lane, the im2col position offsets of the 11 k-steps (p = 4 s + kq)
+    // this wave's tiles: group's range [t0, t1), wave-strided
+    const int t0 = ntiles * group / groups, t1 = ntiles * (group + 1) / groups;
     int pb[11];
     bool pv[11];
 #pragma unroll
@@ -209,48 +227,64 @@ __global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict
         const int pp = pv[s] ? p : 0;
         pb[s] = (pp / kCols + 1) * 9 + pp % kCols + 1;
     }
-    constexpr int G = 4;   // tiles in flight per wave (independent MFMA chains)
-    for (int t0 = wave * G; t0 < ntiles; t0 += 4 * G) {
-        f32x4 acc[G];
-        int cols[G];        // plane base + tap offset (may be negative: c = 0, tap above/left)
-        bool kval[G];       // k < K (past K: the padded tail of the last k tile)
-        const float *arow[G];
+    f32x4 acc[kWgMaxTiles];
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-            acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-            const int t = min(t0 + g, ntiles - 1);
-            const int mt = t / NK, kt = t - mt * NK;
-            arow[g] = ds + (mt * 16 + row) * 44;           // A[m = channel][kk = position]
-            const int k = kt * 16 + row;                   // B[kk = position][n = k]
-            const int tap = k / cinp, c = k - tap * cinp;
-            kval[g] = k < K;
-            cols[g] = kval[g] ? c * kPlane + tap_off(tap) : 0;
+    for (int j = 0; j < kWgMaxTiles; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float accb = 0.f;
+    const int b0 = chunk * kWgSamples, b1 = min(B, b0 + kWgSamples);
+    // the next sample's planes and dz rows are loaded into registers while the
+    // current sample's MFMAs run (one exposed round trip per chunk, not per sample)
+    float vx[kStageMax], vd[kDzMax];
+    load_planes(x + (size_t)b0 * cin * kCells, cin, CINP, vx);
+    load_dz(dz + (size_t)b0 * cout * kCells, cout, coutp, vd);
+    for (int b = b0; b < b1; ++b) {
+        store_planes(vx, CINP, xs);
+        store_dz(vd, coutp, ds);
+        __syncthreads();
+        if (b + 1 < b1) {
+            load_planes(x + (size_t)(b + 1) * cin * kCells, cin, CINP, vx);
+            load_dz(dz + (size_t)(b + 1) * cout * kCells, cout, coutp, vd);
+        }
+        if (group == 0 && threadIdx.x < cout) {   // bias partial (fixed order)
+            float t = 0.f;
+            for (int p = 0; p < kCells; ++p) t += ds[threadIdx.x * 44 + p];
+            accb += t;
         }
 #pragma unroll
-        for (int s = 0; s < 11; ++s) {
+        for (int j = 0; j < kWgMaxTiles; ++j) {
+            const int t = t0 + wave + 4 * j;
+            if (t >= t1) break;
+            const int mt = t / NK, kt = t - mt * NK;
+            const float *arow = ds + (mt * 16 + row) * 44;    // A[m = channel][kk = position]
+            const int k = kt * 16 + row;                      // B[kk = position][n = k]
+            const bool kval = k < K;
+            const int tap = k / CINP, c = k % CINP;           // CINP: compile-time
+            const int col = kval ? c * kPlane + tap_off(tap) : 0;
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const float av = arow[g][4 * s + kq];
-                const float bv = (kval[g] && pv[s]) ? xs[cols[g] + pb[s]] : 0.f;
-                acc[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[g], 0, 0, 0);
+            for (int s = 0; s < 11; ++s) {
+                const float av = arow[4 * s + kq];
+                const float bv = (kval && pv[s]) ? xs[col + pb[s]] : 0.f;
+                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[j], 0, 0, 0);
             }
         }
+        __syncthreads();   // xs / ds are restaged for the next sample
+    }
+    if (group == 0 && threadIdx.x < cout) partb[(size_t)chunk * cout + threadIdx.x] = accb;
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const int t = t0 + g;
-            if (t >= ntiles) break;
-            const int mt = t / NK, kt = t - mt * NK;
-            const int k = kt * 16 + row;
+    for (int j = 0; j < kWgMaxTiles; ++j) {
+        const int t = t0 + wave + 4 * j;
+        if (t >= t1) break;
+        const int mt = t / NK, kt = t - mt * NK;
+        const int k = kt * 16 + row;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int n = mt * 16 + 4 * kq + r;
-                if (n < cout && k < K) part[((size_t)b * cout + n) * K + k] = acc[g][r];
-            }
+        for (int r = 0; r < 4; ++r) {
+            const int n = mt * 16 + 4 * kq + r;
+            if (n < cout && k < K) part[((size_t)chunk * cout + n) * K + k] = acc[j][r];
         }
     }
 }
 
-// dW[n][c][tap] = sum_b part[b][n][tap * cinp + c];  db[n] = sum_b partb[b][n]  (fixed order)
+// dW[n][c][tap] = sum_chunk part[chunk][n][tap * cinp + c];  db[n] = sum_chunk partb[chunk][n]  (fixed order)
 __global__ void k_wgrad_reduce(const float *__restrict__ part, const float *__restrict__ partb, int B, int cin,
                                int cout, float *__restrict__ dw, float *__restrict__ db) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -300,13 +334,23 @@ __global__ __launch_bounds__(kThreads) void k_bn_stats(const float *__restrict__
                                                        float *__restrict__ run_var) {
     __shared__ float red[kThreads];
     const int c = blockIdx.x, n = B * kCells;
+    auto at = [&](int i) { return ((size_t)(i / kCells) * c_n + c) * kCells + i % kCells; };
     float s = 0.f;
-    for (int i = threadIdx.x; i < n; i += kThreads) s += z[((size_t)(i / kCells) * c_n + c) * kCells + i % kCells];
+    for (int i0 = threadIdx.x; i0 < n; i0 += 16 * kThreads) {   // 16 loads in flight, summed in order
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = i0 + j * kThreads < n ? z[at(i0 + j * kThreads)] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) s += v[j];
+    }
     const float mu = block_sum(s, red) / (float)n;
     float q = 0.f;
-    for (int i = threadIdx.x; i < n; i += kThreads) {
-        const float d = z[((size_t)(i / kCells) * c_n + c) * kCells + i % kCells] - mu;
-        q += d * d;
+    for (int i0 = threadIdx.x; i0 < n; i0 += 16 * kThreads) {
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = i0 + j * kThreads < n ? z[at(i0 + j * kThreads)] - mu : 0.f;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) q += v[j] * v[j];
     }
     const float var = block_sum(q, red) / (float)n;
     if (threadIdx.x == 0) {
@@ -339,12 +383,24 @@ __global__ __launch_bounds__(kThreads) void k_bn_bwd(const float *__restrict__ d
     __shared__ float red[kThreads];
     const int c = blockIdx.x, n = B * kCells;
     const float mu = mean[c], is = invstd[c];
+    auto at = [&](int i) { return ((size_t)(i / kCells) * c_n + c) * kCells + i % kCells; };
     float s1 = 0.f, s2 = 0.f;
-    for (int i = threadIdx.x; i < n; i += kThreads) {
-        const size_t k = ((size_t)(i / kCells) * c_n + c) * kCells + i % kCells;
-        const float dy = a[k] > 0.f ? da[k] : 0.f;
-        s1 += dy;
-        s2 += dy * ((z[k] - mu) * is);
+    for (int i0 = threadIdx.x; i0 < n; i0 += 8 * kThreads) {   // 8 x 3 loads in flight, summed in order
+        float vd[8], va[8], vz[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const bool ok = i0 + j * kThreads < n;
+            const size_t k = ok ? at(i0 + j * kThreads) : 0;
+            vd[j] = ok ? da[k] : 0.f;
+            va[j] = ok ? a[k] : 0.f;
+            vz[j] = ok ? z[k] : mu;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float dy = va[j] > 0.f ? vd[j] : 0.f;
+            s1 += dy;
+            s2 += dy * ((vz[j] - mu) * is);
+        }
     }
     const float sb = block_sum(s1, red), sg = block_sum(s2, red);
     if (threadIdx.x == 0) {
@@ -414,7 +470,14 @@ __global__ void k_linear_bwd_w(const float *__restrict__ x, const float *__restr
     if (i < O * K) {
         const int o = i / K, k = i - o * K;
         float s = 0.f;
-        for (int b = 0; b < B; ++b) s += dy[b * O + o] * x[(size_t)b * K + k];
+        for (int b0 = 0; b0 < B; b0 += 16) {   // 16 loads in flight, summed in batch order
+            float v[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v[j] = b0 + j < B ? x[(size_t)(b0 + j) * K + k] : 0.f;
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                if (b0 + j < B) s += dy[(b0 + j) * O + o] * v[j];
+        }
         dw[i] = s;
     }
     if (i < O) {
@@ -535,13 +598,22 @@ int launch_conv(spai_learner *L, const float *in, int cin, const float *w, const
     }
 }
 
-// dW, db of one conv: per-sample partials on f32 MFMA, then a fixed-order sum over the batch
-void launch_wgrad(spai_learner *L, const float *x, int cin, const float *dz, int cout, int B, float *dw, float *db,
-                  hipStream_t st) {
-    const size_t lds = ((size_t)round4(cin) * kPlane + (size_t)round16(cout) * 44) * sizeof(float);
-    k_wgrad_mfma<<<B, kThreads, lds, st>>>(x, cin, dz, cout, L->wpart.p, L->bpart.p);
-    k_wgrad_reduce<<<blocks_of((size_t)cout * 9 * round4(cin)), kThreads, 0, st>>>(L->wpart.p, L->bpart.p, B, cin, cout, dw,
-                                                                          db);
+// dW, db of one conv: chunk partials on f32 MFMA, then a fixed-order sum over the chunks
+int launch_wgrad(spai_learner *L, const float *x, int cin, const float *dz, int cout, int B, float *dw, float *db,
+                 hipStream_t st) {
+    const int cinp = round4(cin), nk = (9 * cinp + 15) / 16, ntiles = (round16(cout) / 16) * nk;
+    const int groups = std::max(1, (ntiles + 4 * kWgMaxTiles - 1) / (4 * kWgMaxTiles));
+    const int chunks = (B + kWgSamples - 1) / kWgSamples;
+    const size_t lds = ((size_t)cinp * kPlane + (size_t)round16(cout) * 44) * sizeof(float);
+    const dim3 grid(chunks, groups);
+    switch (cinp) {
+    case 4: k_wgrad_mfma<4><<<grid, kThreads, lds, st>>>(x, cin, dz, cout, B, groups, L->wpart.p, L->bpart.p); break;
+    case 64: k_wgrad_mfma<64><<<grid, kThreads, lds, st>>>(x, cin, dz, cout, B, groups, L->wpart.p, L->bpart.p); break;
+    default: set_error("learner wgrad: %d input channels not built", cin); return SPAI_ERR_UNSUPPORTED;
+    }
+    k_wgrad_reduce<<<blocks_of((size_t)cout * 9 * cinp), kThreads, 0, st>>>(L->wpart.p, L->bpart.p, chunks, cin, cout,
+                                                                           dw, db);
+    return SPAI_OK;
 }
 
 }  // namespace
@@ -689,7 +761,7 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
         const spai_learner::Conv &c = L->convs[l];
         k_bn_bwd<<<c.co, kThreads, 0, st>>>(da, L->a[l].p, L->z[l].p, c.co, (int)B, L->mean[l].p, L->invstd[l].p,
                                             P + c.g, G + c.g, G + c.be, L->d2.p);
-        launch_wgrad(L, in, c.ci, L->d2.p, c.co, (int)B, G + c.w, G + c.b, st);
+        if (crc == SPAI_OK) crc = launch_wgrad(L, in, c.ci, L->d2.p, c.co, (int)B, G + c.w, G + c.b, st);
         if (dx && crc == SPAI_OK) crc = launch_conv(L, L->d2.p, c.co, P + c.w, nullptr, c.ci, dx, (int)B, acc, true, st);
     };
     bn_conv_bwd(pol, L->d1.p, h, L->d0.p, false);
@@ -710,7 +782,7 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
             const spai_learner::Conv &c = L->convs[l2];
             k_bn_bwd<<<c.co, kThreads, 0, st>>>(L->d1.p, L->a[l2].p, L->z[l2].p, c.co, (int)B, L->mean[l2].p,
                                                 L->invstd[l2].p, P + c.g, G + c.g, G + c.be, L->d2.p);
-            launch_wgrad(L, L->a[l1].p, c.ci, L->d2.p, c.co, (int)B, G + c.w, G + c.b, st);
+            if (crc == SPAI_OK) crc = launch_wgrad(L, L->a[l1].p, c.ci, L->d2.p, c.co, (int)B, G + c.w, G + c.b, st);
             if (crc == SPAI_OK) crc = launch_conv(L, L->d2.p, c.co, P + c.w, nullptr, c.ci, L->d0.p, (int)B, false, true, st);
         }
         // BN1/conv1 backward: da = d0 (gradient wrt relu1 output), mask a[l1]; its input is hin;
