@@ -228,6 +228,17 @@ int spai_learner_grads(spai_learner *l, float *grads, size_t n_params);
 int spai_comm_unique_id(uint8_t *id /* SPAI_COMM_ID_BYTES */);
 int spai_learner_set_comm(spai_learner *l, int rank, int world, const uint8_t *id);
 
+/* ---------------------------------------------------------------- checkpoints
+ * safetensors files with tch VarStore naming (VarStore::save / load,
+ * learner.rs:192, main.rs:61): the flat construction-order parameters <-> one
+ * F32 tensor per variable ("weight", "bias", "weight__2", ... "running_var__5"
+ * ...), shapes as tch (conv [co][ci][3][3], linear [out][in]).  Host-only: no
+ * device needed. */
+int spai_params_save_safetensors(int game, int blocks, int hidden, const float *params, size_t n_params,
+                                 const char *path);
+int spai_params_load_safetensors(int game, int blocks, int hidden, const char *path, float *params,
+                                 size_t n_params);
+
 #ifdef __cplusplus
 }
 #endif

@@ -446,3 +446,16 @@ int spai_learner_set_comm(spai_learner *l, int rank, int world, const uint8_t *i
     if (world > 1) PTR_CHECK(id);   // world 1: an id makes a 1-rank RCCL communicator, NULL none
     return learner_set_comm(l, rank, world, id);
 }
+
+// ---------------------------------------------------------------- checkpoints
+int spai_params_save_safetensors(int game, int blocks, int hidden, const float *params, size_t n, const char *path) {
+    PTR_CHECK(params);
+    PTR_CHECK(path);
+    return params_save_safetensors(game, blocks, hidden, params, n, path);
+}
+
+int spai_params_load_safetensors(int game, int blocks, int hidden, const char *path, float *params, size_t n) {
+    PTR_CHECK(params);
+    PTR_CHECK(path);
+    return params_load_safetensors(game, blocks, hidden, path, params, n);
+}

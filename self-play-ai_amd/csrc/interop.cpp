@@ -1,0 +1,253 @@
+// interop.cpp — safetensors checkpoints with tch VarStore naming.
+//
+// The reference saves and loads its nets with VarStore::save/load
+// (learner.rs:192, learner_concurrent.rs:155-156, main.rs:61).  tch 0.13 keys
+// every variable by its path name on the root path; a name already present
+// gets the suffix "__<number of variables in the store>" (nn::Path::add).
+// Construction order (model/mod.rs:167-184, model/connect_four.rs:54-72):
+// each conv2d adds weight, bias; each batch_norm2d weight, bias, running_mean,
+// running_var; each linear weight, bias — stem, residual blocks, policy head,
+// value head.  tch is not vendored: this naming is restated from its source as
+// recalled (parity unpinned); the file format itself is checked against the
+// safetensors package in the tests.
+//
+// File format: u64 little-endian header length, a JSON header
+// {"name": {"dtype": "F32", "shape": [...], "data_offsets": [begin, end]}, ...}
+// and the raw little-endian tensor bytes.
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "spai_internal.h"
+
+namespace spai {
+namespace {
+
+struct TensorSpec {
+    std::string name;
+    std::vector<int64_t> shape;
+    size_t offset;   // into the flat parameter vector (floats)
+    size_t count;
+};
+
+// the C4 net's variables in construction order, with tch names and shapes
+std::vector<TensorSpec> c4_specs(int blocks, int hidden) {
+    std::vector<TensorSpec> out;
+    std::map<std::string, int> seen;
+    size_t off = 0;
+    auto add = [&](const std::string &base, std::vector<int64_t> shape) {
+        size_t n = 1;
+        for (int64_t d : shape) n *= (size_t)d;
+        std::string name = base;
+        if (seen.count(base)) name = base + "__" + std::to_string(out.size());
+        seen[base] = 1;
+        out.push_back({name, shape, off, n});
+        off += n;
+    };
+    auto conv_bn = [&](int64_t ci, int64_t co) {
+        add("weight", {co, ci, 3, 3});
+        add("bias", {co});
+        add("weight", {co});
+        add("bias", {co});
+        add("running_mean", {co});
+        add("running_var", {co});
+    };
+    conv_bn(3, hidden);
+    for (int b = 0; b < 2 * blocks; ++b) conv_bn(hidden, hidden);
+    conv_bn(hidden, 32);
+    add("weight", {7, 32 * 42});
+    add("bias", {7});
+    conv_bn(hidden, 3);
+    add("weight", {1, 3 * 42});
+    add("bias", {1});
+    return out;
+}
+
+// ---- a minimal JSON reader for the safetensors header (objects, strings, integer arrays)
+struct Json {
+    const char *p, *end;
+    bool ok = true;
+    void ws() {
+        while (p < end && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+    }
+    bool eat(char c) {
+        ws();
+        if (p < end && *p == c) {
+            ++p;
+            return true;
+        }
+        return false;
+    }
+    std::string str() {
+        ws();
+        std::string s;
+        if (p >= end || *p != '"') {
+            ok = false;
+            return s;
+        }
+        ++p;
+        while (p < end && *p != '"') {
+            if (*p == '\\' && p + 1 < end) ++p;
+            s += *p++;
+        }
+        if (p < end) ++p;
+        else ok = false;
+        return s;
+    }
+    int64_t integer() {
+        ws();
+        int64_t v = 0;
+        bool neg = false, any = false;
+        if (p < end && *p == '-') {
+            neg = true;
+            ++p;
+        }
+        while (p < end && *p >= '0' && *p <= '9') {
+            v = v * 10 + (*p++ - '0');
+            any = true;
+        }
+        if (!any) ok = false;
+        return neg ? -v : v;
+    }
+    std::vector<int64_t> int_array() {
+        std::vector<int64_t> v;
+        if (!eat('[')) {
+            ok = false;
+            return v;
+        }
+        if (eat(']')) return v;
+        do v.push_back(integer());
+        while (ok && eat(','));
+        if (!eat(']')) ok = false;
+        return v;
+    }
+    void skip_value() {   // strings, numbers, nested objects/arrays (for __metadata__)
+        ws();
+        if (p >= end) {
+            ok = false;
+            return;
+        }
+        if (*p == '"') {
+            str();
+        } else if (*p == '{' || *p == '[') {
+            const char open = *p, close = open == '{' ? '}' : ']';
+            int depth = 0;
+            do {
+                if (*p == '"') {
+                    str();
+                    continue;
+                }
+                if (*p == open) ++depth;
+                if (*p == close) --depth;
+                ++p;
+            } while (p < end && depth > 0);
+        } else {
+            while (p < end && *p != ',' && *p != '}' && *p != ']') ++p;
+        }
+    }
+};
+
+struct Entry {
+    std::string dtype;
+    std::vector<int64_t> shape;
+    int64_t begin = -1, end = -1;
+};
+
+}  // namespace
+
+int params_save_safetensors(int game, int blocks, int hidden, const float *params, size_t n, const char *path) {
+    SPAI_CHECK(game == SPAI_GAME_CONNECT4, SPAI_ERR_UNSUPPORTED, "safetensors: only the Connect4 net is built");
+    SPAI_CHECK(n == net_num_params(game, blocks, hidden), SPAI_ERR_INVALID, "expected %zu params, got %zu",
+               net_num_params(game, blocks, hidden), n);
+    const std::vector<TensorSpec> specs = c4_specs(blocks, hidden);
+    std::string h = "{\"__metadata__\":{\"format\":\"pt\"}";
+    size_t byte = 0;
+    for (const TensorSpec &t : specs) {
+        h += ",\"" + t.name + "\":{\"dtype\":\"F32\",\"shape\":[";
+        for (size_t i = 0; i < t.shape.size(); ++i) h += (i ? "," : "") + std::to_string(t.shape[i]);
+        h += "],\"data_offsets\":[" + std::to_string(byte) + "," + std::to_string(byte + 4 * t.count) + "]}";
+        byte += 4 * t.count;
+    }
+    h += "}";
+    while ((8 + h.size()) % 8) h += ' ';   // align the data block to 8 bytes (spec allows trailing spaces)
+    FILE *f = std::fopen(path, "wb");
+    SPAI_CHECK(f, SPAI_ERR_INVALID, "cannot open %s for writing", path);
+    const uint64_t hl = h.size();
+    uint8_t le[8];
+    for (int i = 0; i < 8; ++i) le[i] = (uint8_t)(hl >> (8 * i));
+    bool ok = std::fwrite(le, 1, 8, f) == 8 && std::fwrite(h.data(), 1, h.size(), f) == h.size();
+    for (const TensorSpec &t : specs)   // construction order = flat order: one contiguous write
+        ok = ok && std::fwrite(params + t.offset, 4, t.count, f) == t.count;
+    ok = (std::fclose(f) == 0) && ok;
+    SPAI_CHECK(ok, SPAI_ERR_INVALID, "write to %s failed", path);
+    return SPAI_OK;
+}
+
+int params_load_safetensors(int game, int blocks, int hidden, const char *path, float *params, size_t n) {
+    SPAI_CHECK(game == SPAI_GAME_CONNECT4, SPAI_ERR_UNSUPPORTED, "safetensors: only the Connect4 net is built");
+    SPAI_CHECK(n == net_num_params(game, blocks, hidden), SPAI_ERR_INVALID, "expected %zu params, got %zu",
+               net_num_params(game, blocks, hidden), n);
+    FILE *f = std::fopen(path, "rb");
+    SPAI_CHECK(f, SPAI_ERR_INVALID, "cannot open %s", path);
+    std::vector<uint8_t> buf;
+    {
+        uint8_t tmp[1 << 16];
+        size_t r;
+        while ((r = std::fread(tmp, 1, sizeof(tmp), f)) > 0) buf.insert(buf.end(), tmp, tmp + r);
+        std::fclose(f);
+    }
+    SPAI_CHECK(buf.size() >= 8, SPAI_ERR_INVALID, "%s: not a safetensors file", path);
+    uint64_t hl = 0;
+    for (int i = 0; i < 8; ++i) hl |= (uint64_t)buf[i] << (8 * i);
+    SPAI_CHECK(hl <= buf.size() - 8, SPAI_ERR_INVALID, "%s: header length %llu past the end", path,
+               (unsigned long long)hl);
+    const uint8_t *data = buf.data() + 8 + hl;
+    const size_t data_len = buf.size() - 8 - hl;
+    Json js{(const char *)buf.data() + 8, (const char *)buf.data() + 8 + hl};
+    std::map<std::string, Entry> entries;
+    SPAI_CHECK(js.eat('{'), SPAI_ERR_INVALID, "%s: bad header", path);
+    if (!js.eat('}')) {
+        do {
+            const std::string key = js.str();
+            SPAI_CHECK(js.ok && js.eat(':'), SPAI_ERR_INVALID, "%s: bad header near '%s'", path, key.c_str());
+            if (key == "__metadata__") {
+                js.skip_value();
+                continue;
+            }
+            Entry e;
+            SPAI_CHECK(js.eat('{'), SPAI_ERR_INVALID, "%s: bad entry '%s'", path, key.c_str());
+            do {
+                const std::string field = js.str();
+                SPAI_CHECK(js.ok && js.eat(':'), SPAI_ERR_INVALID, "%s: bad entry '%s'", path, key.c_str());
+                if (field == "dtype") e.dtype = js.str();
+                else if (field == "shape") e.shape = js.int_array();
+                else if (field == "data_offsets") {
+                    const std::vector<int64_t> o = js.int_array();
+                    if (o.size() == 2) {
+                        e.begin = o[0];
+                        e.end = o[1];
+                    }
+                } else js.skip_value();
+            } while (js.ok && js.eat(','));
+            SPAI_CHECK(js.ok && js.eat('}'), SPAI_ERR_INVALID, "%s: bad entry '%s'", path, key.c_str());
+            entries[key] = e;
+        } while (js.ok && js.eat(','));
+        SPAI_CHECK(js.ok && js.eat('}'), SPAI_ERR_INVALID, "%s: bad header", path);
+    }
+    for (const TensorSpec &t : c4_specs(blocks, hidden)) {
+        auto it = entries.find(t.name);
+        SPAI_CHECK(it != entries.end(), SPAI_ERR_INVALID, "%s: missing tensor '%s'", path, t.name.c_str());
+        const Entry &e = it->second;
+        SPAI_CHECK(e.dtype == "F32", SPAI_ERR_UNSUPPORTED, "%s: tensor '%s' is %s, expected F32", path,
+                   t.name.c_str(), e.dtype.c_str());
+        SPAI_CHECK(e.shape == t.shape, SPAI_ERR_INVALID, "%s: tensor '%s' has the wrong shape", path, t.name.c_str());
+        SPAI_CHECK(e.begin >= 0 && e.end - e.begin == (int64_t)(4 * t.count) && (size_t)e.end <= data_len,
+                   SPAI_ERR_INVALID, "%s: tensor '%s' has bad data offsets", path, t.name.c_str());
+        memcpy(params + t.offset, data + e.begin, 4 * t.count);   // little-endian F32 on this host
+    }
+    return SPAI_OK;
+}
+
+}  // namespace spai

@@ -208,6 +208,10 @@ int learner_params(spai_learner *l, float *params, size_t n, bool grads);
 int learner_set_comm(spai_learner *l, int rank, int world, const uint8_t *id);
 int comm_unique_id(uint8_t *id);
 
+// interop.cpp
+int params_save_safetensors(int game, int blocks, int hidden, const float *params, size_t n, const char *path);
+int params_load_safetensors(int game, int blocks, int hidden, const char *path, float *params, size_t n);
+
 // search.hip
 int trees_create(spai_engine *e, uint32_t n);
 int tree_reset(spai_engine *e, uint32_t t, const spai_c4_state *root);

@@ -34,7 +34,7 @@ SYMBOLS = [
     "spai_selfplay_run", "spai_engine_set_timing", "spai_engine_timing", "spai_engine_timing_items",
     "spai_net_phase_cycles", "spai_adam_config_default", "spai_learner_create", "spai_learner_destroy",
     "spai_learner_train_batch", "spai_learner_params", "spai_learner_grads", "spai_comm_unique_id",
-    "spai_learner_set_comm",
+    "spai_learner_set_comm", "spai_params_save_safetensors", "spai_params_load_safetensors",
 ]
 COMM_ID_BYTES = 128
 
@@ -124,6 +124,8 @@ def lib():
         L.spai_learner_grads.argtypes = [vp, vp, C.c_size_t]
         L.spai_comm_unique_id.argtypes = [vp]
         L.spai_learner_set_comm.argtypes = [vp, i32, i32, vp]
+        L.spai_params_save_safetensors.argtypes = [i32, i32, i32, vp, C.c_size_t, C.c_char_p]
+        L.spai_params_load_safetensors.argtypes = [i32, i32, i32, C.c_char_p, vp, C.c_size_t]
         _lib = L
     return _lib
 
@@ -405,3 +407,16 @@ def comm_unique_id():
     buf = np.zeros(COMM_ID_BYTES, np.uint8)
     _check(lib().spai_comm_unique_id(_p(buf)))
     return buf.tobytes()
+
+
+def save_params(path, params, blocks, hidden=64, game=GAME_CONNECT4):
+    """flat parameters -> safetensors with tch VarStore names (VarStore::save)"""
+    p = np.ascontiguousarray(params, np.float32)
+    _check(lib().spai_params_save_safetensors(game, blocks, hidden, _p(p), len(p), os.fsencode(path)))
+
+
+def load_params(path, blocks, hidden=64, game=GAME_CONNECT4):
+    """safetensors with tch VarStore names -> flat parameters (VarStore::load)"""
+    out = np.zeros(num_params(blocks, hidden, game), np.float32)
+    _check(lib().spai_params_load_safetensors(game, blocks, hidden, os.fsencode(path), _p(out), len(out)))
+    return out

@@ -1,0 +1,88 @@
+"""safetensors checkpoints with tch VarStore naming, host-only.
+
+The file format is checked against the official `safetensors` package (read
+and write); the tch naming (root-path names, "__<count>" suffix on repeats)
+is restated from tch 0.13, which is not vendored: parity unpinned."""
+import os
+
+import numpy as np
+import pytest
+
+spai = pytest.importorskip("spai")
+st = pytest.importorskip("safetensors.numpy")
+
+
+def expected_names(blocks):
+    names, seen = [], set()
+
+    def add(base):
+        names.append(base + "__%d" % len(names) if base in seen else base)
+        seen.add(base)
+
+    def conv_bn():
+        for b in ("weight", "bias", "weight", "bias", "running_mean", "running_var"):
+            add(b)
+
+    conv_bn()
+    for _ in range(2 * blocks):
+        conv_bn()
+    conv_bn()
+    add("weight")
+    add("bias")
+    conv_bn()
+    add("weight")
+    add("bias")
+    return names
+
+
+@pytest.mark.parametrize("blocks", [0, 2, 6])
+def test_safetensors_roundtrip_and_format(tmp_path, blocks):
+    p = spai.init_params(blocks, 64, seed=blocks + 1)
+    path = str(tmp_path / "ckpt.safetensors")
+    spai.save_params(path, p, blocks)
+    np.testing.assert_array_equal(spai.load_params(path, blocks), p)
+    # the official reader sees tch's names and shapes, in construction order
+    t = st.load_file(path)
+    names = expected_names(blocks)
+    assert set(t) == set(names)
+    flat = np.concatenate([t[n].reshape(-1) for n in names])
+    np.testing.assert_array_equal(flat, p)
+    assert t["weight"].shape == (64, 3, 3, 3)                 # stem conv
+    assert t["running_var"].shape == (64,)
+    last_lin = names[-2]
+    assert t[last_lin].shape == (1, 126)                       # value head linear
+    assert t[names[-2 - 6 - 2]].shape == (7, 1344)             # policy head linear
+
+
+def test_safetensors_load_foreign_file(tmp_path):
+    """a file written by the safetensors package (any tensor order) loads by name"""
+    blocks = 1
+    p = spai.init_params(blocks, 64, seed=3)
+    ref = os.path.join(tmp_path, "ref.safetensors")
+    spai.save_params(ref, p, blocks)
+    t = st.load_file(ref)
+    other = os.path.join(tmp_path, "other.safetensors")
+    st.save_file({k: t[k] for k in sorted(t, reverse=True)}, other, metadata={"format": "pt"})
+    np.testing.assert_array_equal(spai.load_params(other, blocks), p)
+
+
+def test_safetensors_errors(tmp_path):
+    blocks = 1
+    p = spai.init_params(blocks, 64, seed=3)
+    path = str(tmp_path / "a.safetensors")
+    spai.save_params(path, p, blocks)
+    with pytest.raises(spai.SpaiError):           # wrong architecture (missing tensors)
+        spai.load_params(path, 2)
+    t = st.load_file(path)
+    t["weight"] = t["weight"][:32]                 # wrong shape
+    bad = str(tmp_path / "bad.safetensors")
+    st.save_file(t, bad)
+    with pytest.raises(spai.SpaiError):
+        spai.load_params(bad, blocks)
+    t = st.load_file(path)
+    t["bias"] = t["bias"].astype(np.float64)       # wrong dtype
+    st.save_file(t, bad)
+    with pytest.raises(spai.SpaiError):
+        spai.load_params(bad, blocks)
+    with pytest.raises(spai.SpaiError):
+        spai.load_params(str(tmp_path / "missing.safetensors"), blocks)
