@@ -239,6 +239,52 @@ int spai_params_save_safetensors(int game, int blocks, int hidden, const float *
 int spai_params_load_safetensors(int game, int blocks, int hidden, const char *path, float *params,
                                  size_t n_params);
 
+/* ---------------------------------------------------------------- replay + pipeline
+ * Replay ring (learner_concurrent.rs:244-290, capacity batch_size*100 in
+ * main.rs:142): pushes overwrite the oldest samples (push_iter_overwrite),
+ * pops take the oldest n (pop_iter().take(n)).  Samples are one state
+ * encoding [3][6][7], a policy [7] and a value.  Host memory, thread-safe. */
+typedef struct spai_replay spai_replay;
+int spai_replay_create(uint32_t capacity, spai_replay **out);
+int spai_replay_destroy(spai_replay *r);
+int spai_replay_push(spai_replay *r, uint32_t n, const float *states, const float *policies, const float *values);
+/* SPAI_ERR_INVALID when fewer than n samples are buffered (non-blocking) */
+int spai_replay_pop(spai_replay *r, uint32_t n, float *states, float *policies, float *values);
+int spai_replay_size(spai_replay *r, uint32_t *n);
+/* choose_multiple: k distinct indices of [0, n) from the Philox stream (seed, stream) */
+int spai_choose_multiple(uint32_t n, uint32_t k, uint64_t seed, uint64_t stream, uint32_t *out);
+
+/* train_concurrent (main.rs:137-235): n_selfplay self-play workers (host
+ * threads, one engine each on selfplay_devices[w]) loop while training: take
+ * the latest published weights, play games_per_batch games, push a random
+ * sample_fraction of the positions into the replay ring.  The learner (on
+ * learner_device) runs train_iters x batches_per_iter train steps of
+ * batch_size popped samples, then publishes its weights and, if
+ * checkpoint_dir is set, saves {checkpoint_dir}/{iter}.safetensors.
+ * Reference defaults (SelfPlayArgs / TrainingArgs / C4 Args): c 2, 600 sims,
+ * T 1.25, 100 games, batch 128, 20 batches x 10 iters, capacity 12800,
+ * fraction 0.3, 4 blocks. */
+typedef struct spai_pipeline_config {
+    uint32_t n_selfplay;
+    const int *selfplay_devices;   /* [n_selfplay] */
+    int learner_device;
+    uint32_t games_per_batch, num_searches;
+    float c, temperature;
+    uint32_t batch_size, batches_per_iter, train_iters, replay_capacity;
+    float sample_fraction;
+    int blocks;
+    uint64_t seed;
+    const char *checkpoint_dir;    /* NULL: no checkpoints */
+} spai_pipeline_config;
+typedef struct spai_pipeline_stats {
+    double games, positions, samples_pushed, samples_overwritten, batches_trained;
+    double last_loss[3];
+    double weight_version_published, weight_version_used_max, seconds;
+} spai_pipeline_stats;
+int spai_pipeline_config_default(spai_pipeline_config *cfg);
+int spai_pipeline_run(const spai_pipeline_config *cfg, const float *init_params, size_t n_params,
+                      spai_pipeline_stats *stats);
+
 #ifdef __cplusplus
 }
 #endif

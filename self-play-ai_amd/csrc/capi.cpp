@@ -459,3 +459,77 @@ int spai_params_load_safetensors(int game, int blocks, int hidden, const char *p
     PTR_CHECK(path);
     return params_load_safetensors(game, blocks, hidden, path, params, n);
 }
+
+// ---------------------------------------------------------------- replay + pipeline
+int spai_replay_create(uint32_t capacity, spai_replay **out) {
+    PTR_CHECK(out);
+    return replay_create(capacity, out);
+}
+
+int spai_replay_destroy(spai_replay *r) {
+    if (r) replay_destroy(r);
+    return SPAI_OK;
+}
+
+int spai_replay_push(spai_replay *r, uint32_t n, const float *states, const float *policies, const float *values) {
+    PTR_CHECK(r);
+    if (n) {
+        PTR_CHECK(states);
+        PTR_CHECK(policies);
+        PTR_CHECK(values);
+    }
+    return replay_push(r, n, states, policies, values);
+}
+
+int spai_replay_pop(spai_replay *r, uint32_t n, float *states, float *policies, float *values) {
+    PTR_CHECK(r);
+    if (n) {
+        PTR_CHECK(states);
+        PTR_CHECK(policies);
+        PTR_CHECK(values);
+    }
+    return replay_pop_now(r, n, states, policies, values);
+}
+
+int spai_replay_size(spai_replay *r, uint32_t *n) {
+    PTR_CHECK(r);
+    PTR_CHECK(n);
+    return replay_size(r, n);
+}
+
+int spai_choose_multiple(uint32_t n, uint32_t k, uint64_t seed, uint64_t stream, uint32_t *out) {
+    PTR_CHECK(out);
+    std::vector<uint32_t> v;
+    choose_multiple(n, k, seed, stream, v);
+    std::copy(v.begin(), v.end(), out);
+    return SPAI_OK;
+}
+
+int spai_pipeline_config_default(spai_pipeline_config *cfg) {
+    PTR_CHECK(cfg);
+    static const int dev0 = 0;
+    *cfg = spai_pipeline_config{};
+    cfg->n_selfplay = 1;
+    cfg->selfplay_devices = &dev0;
+    cfg->learner_device = 0;
+    cfg->games_per_batch = 100;   // SelfPlayArgs::default (learner_concurrent.rs:50-59)
+    cfg->num_searches = 600;
+    cfg->c = 2.0f;
+    cfg->temperature = 1.25f;
+    cfg->batch_size = 128;        // TrainingArgs::default (:61-69)
+    cfg->batches_per_iter = 20;
+    cfg->train_iters = 10;
+    cfg->replay_capacity = 128 * 100;   // main.rs:142
+    cfg->sample_fraction = 0.3f;        // learner_concurrent.rs:278
+    cfg->blocks = 4;                    // model::connect_four::Args::default
+    cfg->seed = 0;
+    cfg->checkpoint_dir = nullptr;
+    return SPAI_OK;
+}
+
+int spai_pipeline_run(const spai_pipeline_config *cfg, const float *init_params, size_t n_params,
+                      spai_pipeline_stats *stats) {
+    PTR_CHECK(cfg);
+    PTR_CHECK(init_params);
+    return pipeline_run(cfg, init_params, n_params, stats);
+}

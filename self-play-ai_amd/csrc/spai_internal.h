@@ -212,6 +212,15 @@ int comm_unique_id(uint8_t *id);
 int params_save_safetensors(int game, int blocks, int hidden, const float *params, size_t n, const char *path);
 int params_load_safetensors(int game, int blocks, int hidden, const char *path, float *params, size_t n);
 
+// pipeline.cpp
+int replay_create(uint32_t capacity, spai_replay **out);
+void replay_destroy(spai_replay *r);
+int replay_push(spai_replay *r, uint32_t n, const float *s, const float *p, const float *v);
+int replay_pop_now(spai_replay *r, uint32_t n, float *s, float *p, float *v);
+int replay_size(spai_replay *r, uint32_t *n);
+void choose_multiple(uint32_t n, uint32_t k, uint64_t seed, uint64_t stream, std::vector<uint32_t> &out);
+int pipeline_run(const spai_pipeline_config *cfg, const float *init_params, size_t n_params, spai_pipeline_stats *st);
+
 // search.hip
 int trees_create(spai_engine *e, uint32_t n);
 int tree_reset(spai_engine *e, uint32_t t, const spai_c4_state *root);

@@ -35,6 +35,8 @@ SYMBOLS = [
     "spai_net_phase_cycles", "spai_adam_config_default", "spai_learner_create", "spai_learner_destroy",
     "spai_learner_train_batch", "spai_learner_params", "spai_learner_grads", "spai_comm_unique_id",
     "spai_learner_set_comm", "spai_params_save_safetensors", "spai_params_load_safetensors",
+    "spai_replay_create", "spai_replay_destroy", "spai_replay_push", "spai_replay_pop", "spai_replay_size",
+    "spai_choose_multiple", "spai_pipeline_config_default", "spai_pipeline_run",
 ]
 COMM_ID_BYTES = 128
 
@@ -61,6 +63,21 @@ class SelfPlayStats(C.Structure):
 
 class AdamConfig(C.Structure):
     _fields_ = [(k, C.c_float) for k in ("lr", "beta1", "beta2", "eps", "bn_momentum", "bn_eps")]
+
+
+class PipelineConfig(C.Structure):
+    _fields_ = [("n_selfplay", C.c_uint32), ("selfplay_devices", C.POINTER(C.c_int)), ("learner_device", C.c_int),
+                ("games_per_batch", C.c_uint32), ("num_searches", C.c_uint32), ("c", C.c_float),
+                ("temperature", C.c_float), ("batch_size", C.c_uint32), ("batches_per_iter", C.c_uint32),
+                ("train_iters", C.c_uint32), ("replay_capacity", C.c_uint32), ("sample_fraction", C.c_float),
+                ("blocks", C.c_int), ("seed", C.c_uint64), ("checkpoint_dir", C.c_char_p)]
+
+
+class PipelineStats(C.Structure):
+    _fields_ = [(k, C.c_double) for k in ("games", "positions", "samples_pushed", "samples_overwritten",
+                                          "batches_trained")] + \
+               [("last_loss", C.c_double * 3)] + \
+               [(k, C.c_double) for k in ("weight_version_published", "weight_version_used_max", "seconds")]
 
 
 SINK = C.CFUNCTYPE(None, C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_float), C.POINTER(C.c_float),
@@ -126,6 +143,14 @@ def lib():
         L.spai_learner_set_comm.argtypes = [vp, i32, i32, vp]
         L.spai_params_save_safetensors.argtypes = [i32, i32, i32, vp, C.c_size_t, C.c_char_p]
         L.spai_params_load_safetensors.argtypes = [i32, i32, i32, C.c_char_p, vp, C.c_size_t]
+        L.spai_replay_create.argtypes = [u32, P(vp)]
+        L.spai_replay_destroy.argtypes = [vp]
+        L.spai_replay_push.argtypes = [vp, u32, vp, vp, vp]
+        L.spai_replay_pop.argtypes = [vp, u32, vp, vp, vp]
+        L.spai_replay_size.argtypes = [vp, P(u32)]
+        L.spai_choose_multiple.argtypes = [u32, u32, u64, u64, vp]
+        L.spai_pipeline_config_default.argtypes = [P(PipelineConfig)]
+        L.spai_pipeline_run.argtypes = [P(PipelineConfig), vp, C.c_size_t, P(PipelineStats)]
         _lib = L
     return _lib
 
@@ -419,4 +444,58 @@ def load_params(path, blocks, hidden=64, game=GAME_CONNECT4):
     """safetensors with tch VarStore names -> flat parameters (VarStore::load)"""
     out = np.zeros(num_params(blocks, hidden, game), np.float32)
     _check(lib().spai_params_load_safetensors(game, blocks, hidden, os.fsencode(path), _p(out), len(out)))
+    return out
+
+
+class Replay:
+    """replay ring (HeapRb, push_iter_overwrite / pop_iter().take(n))"""
+
+    def __init__(self, capacity):
+        self.h = C.c_void_p()
+        _check(lib().spai_replay_create(capacity, C.byref(self.h)))
+
+    def push(self, states, policies, values):
+        s = np.ascontiguousarray(states, np.float32).reshape(-1, 126)
+        p = np.ascontiguousarray(policies, np.float32).reshape(-1, 7)
+        v = np.ascontiguousarray(values, np.float32).reshape(-1)
+        _check(lib().spai_replay_push(self.h, len(v), _p(s), _p(p), _p(v)))
+
+    def pop(self, n):
+        s, p, v = np.zeros((n, 126), np.float32), np.zeros((n, 7), np.float32), np.zeros(n, np.float32)
+        _check(lib().spai_replay_pop(self.h, n, _p(s), _p(p), _p(v)))
+        return s, p, v
+
+    def __len__(self):
+        n = C.c_uint32()
+        _check(lib().spai_replay_size(self.h, C.byref(n)))
+        return n.value
+
+    def close(self):
+        if self.h:
+            lib().spai_replay_destroy(self.h)
+            self.h = C.c_void_p()
+
+
+def choose_multiple(n, k, seed=0, stream=0):
+    out = np.zeros(min(n, k), np.uint32)
+    _check(lib().spai_choose_multiple(n, k, seed, stream, _p(out)))
+    return out
+
+
+def pipeline_run(init_params, selfplay_devices=(0,), learner_device=0, checkpoint_dir=None, **kw):
+    """train_concurrent (main.rs:137-235) on the device; kw: PipelineConfig fields"""
+    cfg = PipelineConfig()
+    _check(lib().spai_pipeline_config_default(C.byref(cfg)))
+    devs = (C.c_int * len(selfplay_devices))(*selfplay_devices)
+    cfg.n_selfplay = len(selfplay_devices)
+    cfg.selfplay_devices = devs
+    cfg.learner_device = learner_device
+    cfg.checkpoint_dir = os.fsencode(checkpoint_dir) if checkpoint_dir else None
+    for k, v in kw.items():
+        setattr(cfg, k, v)
+    p = np.ascontiguousarray(init_params, np.float32)
+    st = PipelineStats()
+    _check(lib().spai_pipeline_run(C.byref(cfg), _p(p), len(p), C.byref(st)))
+    out = {k: getattr(st, k) for k, _ in PipelineStats._fields_ if k != "last_loss"}
+    out["last_loss"] = list(st.last_loss)
     return out

@@ -455,3 +455,24 @@ def test_learner_rccl_single_rank(spai):
         e.close()
     np.testing.assert_array_equal(out[0][0], out[1][0])
     np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
+# ------------------------------------------------------------------ pipeline
+def test_pipeline_concurrent(spai, tmp_path):
+    """train_concurrent (main.rs:137-235) end to end on one GPU: a self-play worker
+    thread feeding the replay ring, the learner training batches from it, weights
+    published per iteration and picked up by self-play, checkpoints written"""
+    blocks = 1
+    p0 = spai.init_params(blocks, 64, seed=11)
+    st = spai.pipeline_run(p0, selfplay_devices=(0,), learner_device=0, checkpoint_dir=str(tmp_path),
+                           games_per_batch=32, num_searches=16, batch_size=32, batches_per_iter=3, train_iters=3,
+                           replay_capacity=320, blocks=blocks, seed=2)
+    assert st["batches_trained"] == 9
+    assert st["weight_version_published"] == 3
+    assert st["games"] >= 32 and st["positions"] > 0
+    assert st["samples_pushed"] == pytest.approx(st["samples_pushed"])
+    assert all(np.isfinite(st["last_loss"])) and st["last_loss"][0] > 0
+    for it in range(3):
+        p = spai.load_params(str(tmp_path / ("%d.safetensors" % it)), blocks)
+        assert p.shape == p0.shape and np.isfinite(p).all()
+    assert not np.array_equal(spai.load_params(str(tmp_path / "2.safetensors"), blocks), p0)
