@@ -244,7 +244,11 @@ __device__ __forceinline__ void conv_mfma(const uint8_t *smem, const Geo<Plan<W,
 #pragma unroll
     for (int ks = 0; ks < kKStepsRes; ++ks) {
         constexpr int la = DA - 1, lb = DB - 1;
+#ifdef SPAI_EXP_NO_A
+        if (false) {
+#else
         if (ks + la < kKStepsRes) {
+#endif
 #pragma unroll
             for (int c = 0; c < CTL; ++c)
 #ifdef SPAI_EXP_A_FIXED
@@ -253,8 +257,10 @@ __device__ __forceinline__ void conv_mfma(const uint8_t *smem, const Geo<Plan<W,
                 A[(ks + la) % DA][c] = wl[((ks + la) * CT + c) * 64];
 #endif
         } else {
+#ifndef SPAI_EXP_NO_A
 #pragma unroll
             for (int c = 0; c < CTL; ++c) A[(ks + la) % DA][c] = wnl[((ks + la - kKStepsRes) * CT + c) * 64];
+#endif
         }
         if (ks + lb < kKStepsRes) {
             const int tap = (ks + lb) >> 1, flip = ((ks + lb) & 1) << 6;

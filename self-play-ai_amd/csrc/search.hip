@@ -247,14 +247,20 @@ BatchView batch_view(spai_engine *e, int chain, uint32_t slot) {
 }
 
 // Number of search chains for n trees: two halves when each half still fills
-// a useful batch (SPAI_CHAINS=k forces up to k chains, for A/B measurements).
-int chains_for(uint32_t n) {
+// a useful batch.  Late in a game most trees are solved and an iteration
+// evaluates almost nothing; then the second chain only doubles the launches,
+// so one chain is used when the previous search call averaged fewer than
+// kMinChainLeaves leaves per iteration.  (SPAI_CHAINS=k forces up to k chains,
+// for A/B measurements.)  The split never changes results: trees are independent.
+constexpr double kMinChainLeaves = 64;
+int chains_for(uint32_t n, double last_evals_per_iter) {
     static const int forced = [] {
         const char *v = std::getenv("SPAI_CHAINS");
         return v ? std::max(1, std::min(spai_engine::kChains, std::atoi(v))) : 0;
     }();
-    const int want = forced ? forced : 2;
-    return std::max(1, std::min<int>(want, (int)(n / 64)));
+    if (forced) return std::max(1, std::min<int>(forced, (int)(n / 64)));
+    if (last_evals_per_iter >= 0 && last_evals_per_iter < kMinChainLeaves) return 1;
+    return std::max(1, std::min<int>(2, (int)(n / 64)));
 }
 
 // upload host root bookkeeping for trees [t0, t0+n)
@@ -353,6 +359,7 @@ int trees_create(spai_engine *e, uint32_t n) {
         T.n_trees = n;
         T.cap = (uint32_t)cap;
     }
+    e->last_evals_per_iter = -1;   // a fresh set of trees: no per-iteration statistics yet
     T.h_root.assign(n, 0);
     T.h_root_state.assign(n, c4::State{0, 0, 0, c4::kOngoing});
     T.h_root_first.assign(n, 0);
@@ -391,7 +398,7 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
     if (n == 0) return SPAI_OK;
     hipStream_t st = e->stream;
     // chain h searches active[off[h] .. off[h] + cnt[h]) on chain_stream[h]
-    const int nchain = chains_for(n);
+    const int nchain = chains_for(n, e->last_evals_per_iter);
     uint32_t off[spai_engine::kChains] = {0, 0, 0, 0}, cnt[spai_engine::kChains] = {0, 0, 0, 0};
     for (int h = 0; h < nchain; ++h) {
         off[h] = (uint32_t)((uint64_t)n * h / nchain);
@@ -456,10 +463,11 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
     SPAI_CHECK(!(err & kErrCapacity), SPAI_ERR_CAPACITY, "node arena full (cap %u per tree)", T.cap);
     SPAI_CHECK(!(err & kErrDepth), SPAI_ERR_CAPACITY, "tree deeper than %d", kMaxDepth);
     SPAI_CHECK(!(err & kErrNan), SPAI_ERR_NAN, "NaN UCB in select (reference: partial_cmp().unwrap() panics)");
-    if (evals_out) {
+    {
         double s = 0;
         for (uint32_t c : counts) s += c;
-        *evals_out = s;
+        if (evals_out) *evals_out = s;
+        e->last_evals_per_iter = num_searches ? s / num_searches : -1;
     }
     // root visit policy (mcts.rs:310-331)
     for (uint32_t i = 0; i < n; ++i) {

@@ -166,6 +166,7 @@ struct spai_engine {
     spai::Batch batch[kChains];
     hipStream_t chain_stream[kChains] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join[kChains] = {nullptr, nullptr, nullptr, nullptr};
+    double last_evals_per_iter = -1;   // previous search call's mean leaves per iteration (< 0: none yet)
     spai_net *net = nullptr;
     spai::DevBuf<uint32_t> active;   // active tree list
     spai::DevBuf<uint32_t> err;      // device error flags
