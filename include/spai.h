@@ -217,6 +217,11 @@ int spai_learner_destroy(spai_learner *l);
  * policies [n][7], values [n]; loss[3] = total, policy, value (may be NULL) */
 int spai_learner_train_batch(spai_learner *l, uint32_t n, const float *states, const float *policies,
                              const float *values, float *loss);
+/* Model::train (model/mod.rs:100-149): a fresh Adam, one random permutation of
+ * the n samples (keyed by seed), then `epochs` passes of ceil(n / batch) train
+ * steps (the last batch may be short); loss[3] = the last step's */
+int spai_learner_train(spai_learner *l, uint32_t n, const float *states, const float *policies, const float *values,
+                       uint32_t epochs, uint32_t batch, uint64_t seed, float *loss);
 /* current parameters (incl. BN running statistics) / last step's gradients
  * (after the cross-rank reduction, before the 1/world scale), flat order */
 int spai_learner_params(spai_learner *l, float *params, size_t n_params);

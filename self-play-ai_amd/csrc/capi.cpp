@@ -533,3 +533,13 @@ int spai_pipeline_run(const spai_pipeline_config *cfg, const float *init_params,
     PTR_CHECK(init_params);
     return pipeline_run(cfg, init_params, n_params, stats);
 }
+
+int spai_learner_train(spai_learner *l, uint32_t n, const float *states, const float *policies, const float *values,
+                       uint32_t epochs, uint32_t batch, uint64_t seed, float *loss) {
+    PTR_CHECK(l);
+    PTR_CHECK(states);
+    PTR_CHECK(policies);
+    PTR_CHECK(values);
+    ENG_CHECK(l->eng);
+    return learner_train_epochs(l, n, states, policies, values, epochs, batch, seed, loss);
+}

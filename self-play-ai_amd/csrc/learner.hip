@@ -835,6 +835,35 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
     return SPAI_OK;
 }
 
+// Model::train (model/mod.rs:100-149): a fresh Adam (the reference builds the
+// optimizer inside train), one permutation of the n samples (Tensor::randperm,
+// here a Philox-keyed Fisher-Yates), then `epochs` passes of ceil(n / batch)
+// train steps over the permuted samples (the last batch may be short).
+int learner_train_epochs(spai_learner *L, uint32_t n, const float *states, const float *policies,
+                         const float *values, uint32_t epochs, uint32_t batch, uint64_t seed, float *loss3) {
+    SPAI_CHECK(n >= 1 && batch >= 1, SPAI_ERR_INVALID, "train: need samples and a batch size");
+    hipStream_t st = L->eng->stream;
+    SPAI_HIP(hipMemsetAsync(L->m.p, 0, L->n_params * 4, st));   // Adam::default().build(..) per call
+    SPAI_HIP(hipMemsetAsync(L->v.p, 0, L->n_params * 4, st));
+    L->step = 0;
+    std::vector<uint32_t> perm;
+    choose_multiple(n, n, seed, 0x7EA1Bull, perm);   // a full random permutation
+    std::vector<float> s((size_t)batch * 126), p((size_t)batch * 7), v(batch);
+    const uint32_t nb = (n + batch - 1) / batch;
+    for (uint32_t ep = 0; ep < epochs; ++ep)
+        for (uint32_t b = 0; b < nb; ++b) {
+            const uint32_t lo = b * batch, m = std::min(batch, n - lo);
+            for (uint32_t i = 0; i < m; ++i) {
+                const uint32_t j = perm[lo + i];
+                memcpy(&s[(size_t)i * 126], states + (size_t)j * 126, 126 * 4);
+                memcpy(&p[(size_t)i * 7], policies + (size_t)j * 7, 7 * 4);
+                v[i] = values[j];
+            }
+            SPAI_TRY(learner_train_batch(L, m, s.data(), p.data(), v.data(), loss3));
+        }
+    return SPAI_OK;
+}
+
 int learner_params(spai_learner *L, float *params, size_t n, bool grads) {
     SPAI_CHECK(n == L->n_params, SPAI_ERR_INVALID, "expected %zu params, got %zu", L->n_params, n);
     hipStream_t st = L->eng->stream;

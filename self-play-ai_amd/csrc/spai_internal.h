@@ -206,6 +206,8 @@ void learner_destroy(spai_learner *l);
 int learner_train_batch(spai_learner *l, uint32_t n, const float *states, const float *policies, const float *values,
                         float *loss3);
 int learner_params(spai_learner *l, float *params, size_t n, bool grads);
+int learner_train_epochs(spai_learner *l, uint32_t n, const float *states, const float *policies, const float *values,
+                         uint32_t epochs, uint32_t batch, uint64_t seed, float *loss3);
 int learner_set_comm(spai_learner *l, int rank, int world, const uint8_t *id);
 int comm_unique_id(uint8_t *id);
 

@@ -36,7 +36,7 @@ SYMBOLS = [
     "spai_learner_train_batch", "spai_learner_params", "spai_learner_grads", "spai_comm_unique_id",
     "spai_learner_set_comm", "spai_params_save_safetensors", "spai_params_load_safetensors",
     "spai_replay_create", "spai_replay_destroy", "spai_replay_push", "spai_replay_pop", "spai_replay_size",
-    "spai_choose_multiple", "spai_pipeline_config_default", "spai_pipeline_run",
+    "spai_choose_multiple", "spai_pipeline_config_default", "spai_pipeline_run", "spai_learner_train",
 ]
 COMM_ID_BYTES = 128
 
@@ -139,6 +139,7 @@ def lib():
         L.spai_learner_train_batch.argtypes = [vp, u32, vp, vp, vp, vp]
         L.spai_learner_params.argtypes = [vp, vp, C.c_size_t]
         L.spai_learner_grads.argtypes = [vp, vp, C.c_size_t]
+        L.spai_learner_train.argtypes = [vp, u32, vp, vp, vp, u32, u32, u64, vp]
         L.spai_comm_unique_id.argtypes = [vp]
         L.spai_learner_set_comm.argtypes = [vp, i32, i32, vp]
         L.spai_params_save_safetensors.argtypes = [i32, i32, i32, vp, C.c_size_t, C.c_char_p]
@@ -407,6 +408,15 @@ class Learner:
         loss = np.zeros(3, np.float32)
         _check(lib().spai_learner_train_batch(self.h, len(x), _p(x), _p(pi), _p(z), _p(loss)))
         return loss   # total, policy, value
+
+    def train(self, states, policies, values, epochs=1, batch=128, seed=0):
+        """Model::train (model/mod.rs:100-149): fresh Adam, one permutation, epochs x batches"""
+        x = np.ascontiguousarray(states, np.float32).reshape(-1, 126)
+        pi = np.ascontiguousarray(policies, np.float32).reshape(-1, 7)
+        z = np.ascontiguousarray(values, np.float32).reshape(-1)
+        loss = np.zeros(3, np.float32)
+        _check(lib().spai_learner_train(self.h, len(z), _p(x), _p(pi), _p(z), epochs, batch, seed, _p(loss)))
+        return loss
 
     def params(self):
         out = np.zeros(self.n, np.float32)

@@ -476,3 +476,35 @@ def test_pipeline_concurrent(spai, tmp_path):
         p = spai.load_params(str(tmp_path / ("%d.safetensors" % it)), blocks)
         assert p.shape == p0.shape and np.isfinite(p).all()
     assert not np.array_equal(spai.load_params(str(tmp_path / "2.safetensors"), blocks), p0)
+
+
+def test_learner_model_train_epochs(spai, oracle):
+    """Model::train (model/mod.rs:100-149): a fresh Adam per call, one permutation of
+    the samples, epochs x ceil(n/B) steps (short last batch) — vs the numpy oracle
+    fed the same permutation"""
+    import learner_ref as LR
+    from test_oracle_golden import check_learner_params
+    blocks, n, B, epochs, seed = 1, 70, 32, 2, 9
+    rng = np.random.default_rng(4)
+    states = _reachable_positions(spai, 3 * n, 8, seed=13)[:n]
+    e = spai.Engine(num_searches=1, max_trees=1)
+    e.games_resize(n)
+    e.games_write(states)
+    x = e.encode(n).reshape(n, 126)
+    pi = rng.random((n, 7)).astype(np.float32)
+    pi /= pi.sum(1, keepdims=True)
+    z = rng.choice(np.array([-1, 0, 1], np.float32), n)
+    p0 = spai.init_params(blocks, 64, seed=5)
+    L = spai.Learner(e, blocks, p0)
+    L.train(x, pi, z, epochs=epochs, batch=B, seed=seed)
+    L.train(x, pi, z, epochs=1, batch=B, seed=seed + 1)   # second call: Adam starts over
+    P = L.params()
+    ref, all_grads = p0.astype(np.float64), []
+    for s_, ep in ((seed, epochs), (seed + 1, 1)):
+        perm = spai.choose_multiple(n, n, seed=s_, stream=0x7EA1B).astype(np.int64)
+        batches = [(x[perm[i:i + B]], pi[perm[i:i + B]], z[perm[i:i + B]]) for i in range(0, n, B)] * ep
+        ref, _, grads = LR.train(ref, batches, blocks, 64)
+        all_grads += grads
+    check_learner_params(P, ref, all_grads, blocks, 64, len(all_grads), tol=2e-4)
+    L.close()
+    e.close()
