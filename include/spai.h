@@ -290,6 +290,103 @@ int spai_pipeline_config_default(spai_pipeline_config *cfg);
 int spai_pipeline_run(const spai_pipeline_config *cfg, const float *init_params, size_t n_params,
                       spai_pipeline_stats *stats);
 
+
+/* ---------------------------------------------------------------- chess
+ * game/chess.rs (the adapter over the `chess` crate 3.2.0) on the device:
+ * config 4 of BASELINE.json.  A separate engine type: a position is a set of
+ * bitboards, a move is a 16-bit code, the policy has 73*8*8 = 4672 entries
+ * (chess.rs:252-257), the encoding is [19][8][8] (chess.rs:176-249).
+ *
+ * Move code: src | dst << 6 | promo << 12; squares rank*8 + file (a1 = 0);
+ * promo = 1 knight, 2 bishop, 3 rook, 4 queen (chess::Piece index), 0 none.
+ * Move lists are in MoveGen::new_legal enumeration order (piece type P, N, B,
+ * R, Q, K; unpinned sources before pinned ones; en-passant captures after the
+ * pawns; destinations ascending; promotions Q, N, R, B).  The reference's
+ * repetition count compares these ordered lists (chess.rs:51-61); the device
+ * compares 64-bit hashes of them. */
+#define SPAI_CHESS_POLICY 4672
+#define SPAI_CHESS_ENC 1216
+#define SPAI_CHESS_MAX_MOVES 256
+
+typedef struct spai_chess_state {
+    uint64_t pieces[6];   /* Pawn, Knight, Bishop, Rook, Queen, King (chess::Piece order) */
+    uint64_t colors[2];   /* White, Black */
+    uint8_t side;         /* 0 White to move, 1 Black */
+    uint8_t castle;       /* 1 white kingside, 2 white queenside, 4 black kingside, 8 black queenside */
+    uint8_t ep;           /* chess::Board::en_passant: square of the pawn that just double-pushed, 64 = none */
+    uint8_t status;       /* spai_status (filled by reads) */
+    uint16_t fifty;       /* fifty_move_rule_halfmove_counter (chess.rs:29) */
+    uint16_t made;        /* Action::MakeMove count of the Game (chess.rs:243-246) */
+    uint32_t reps;        /* get_num_repetitions (chess.rs:51-61; filled by reads) */
+    uint32_t pad;
+} spai_chess_state;
+
+typedef struct spai_chess spai_chess;
+typedef struct spai_chess_net spai_chess_net;
+
+/* cfg.max_moves = longest game (sizes the transposition tables; default 2048) */
+int spai_chess_config_default(spai_config *cfg);
+int spai_chess_create(const spai_config *cfg, int device, spai_chess **out);
+int spai_chess_destroy(spai_chess *e);
+int spai_chess_sync(spai_chess *e);
+
+/* rules over n engine-held slots, each with its own transposition table */
+int spai_chess_games_resize(spai_chess *e, uint32_t n);                  /* n x State::default() */
+int spai_chess_games_write(spai_chess *e, uint32_t first, uint32_t n, const spai_chess_state *s); /* empty table */
+int spai_chess_games_read(spai_chess *e, uint32_t first, uint32_t n, spai_chess_state *s);
+/* get_valid_actions (chess.rs:148): moves [n][SPAI_CHESS_MAX_MOVES], counts [n] */
+int spai_chess_legal_moves(spai_chess *e, uint32_t first, uint32_t n, uint16_t *moves, uint32_t *counts);
+/* get_next_state (chess.rs:108-146) in place: rc SPAI_ERR_GAME_OVER ("Game is already
+ * over") or SPAI_ERR_ILLEGAL_MOVE ("Failed to make move"); the slot is unchanged on error */
+int spai_chess_apply(spai_chess *e, uint32_t first, uint32_t n, const uint16_t *moves, int32_t *rc);
+/* get_status (chess.rs:150-166) and get_num_repetitions; get_value_and_terminated
+ * (chess.rs:168-174: Won -> +1, quirk Q7).  Any output may be NULL. */
+int spai_chess_status(spai_chess *e, uint32_t first, uint32_t n, uint8_t *status, uint32_t *reps, float *value,
+                      uint8_t *terminated);
+/* get_encoding: out [n][19][8][8] f32 */
+int spai_chess_encode(spai_chess *e, uint32_t first, uint32_t n, float *out);
+/* mask_invalid_actions (chess.rs:252-275): policy [n][len] -> out [n][4672]; len must be 4672 */
+int spai_chess_mask_invalid(spai_chess *e, uint32_t first, uint32_t n, const float *policy, uint32_t len,
+                            float *out);
+/* Policy::get_prob / set_prob flat index of a move (get_channel, chess.rs:311-393) */
+int spai_chess_move_index(int side, uint16_t move, int32_t *index);
+/* Policy::get_action (chess.rs:395-493), including its knight-underpromotion bug (:442) */
+int spai_chess_index_move(int side, int32_t index, uint16_t *move);
+
+/* net: model/chess.rs:48-77 (torso = stem + `blocks` residual blocks of 256
+ * channels; policy head conv1x1 256->256 + ReLU + conv1x1 256->73; value head
+ * conv1x1 256->1 + ReLU + linear 64->256 + ReLU + linear 256->1 + tanh).  params
+ * in tch construction order as for spai_net_create.  bf16 MFMA, fp32 accumulate. */
+int spai_chess_net_num_params(int blocks, size_t *count);
+int spai_chess_net_init_params(int blocks, uint64_t seed, float *params);
+int spai_chess_net_create(spai_chess *e, int blocks, const float *params, size_t n_params, spai_chess_net **out);
+int spai_chess_net_destroy(spai_chess_net *net);
+/* Net::forward(x, train=false): x [n][19][8][8] -> logits [n][4672], value [n] */
+int spai_chess_net_forward(spai_chess_net *net, uint32_t n, const float *x, float *logits, float *value);
+int spai_chess_set_net(spai_chess *e, spai_chess_net *net);
+
+/* search: Tree (mcts.rs) + Mcts::search over chess trees held on the device.
+ * Per tree i: policy [i][4672] normalized root visits (NULL allowed),
+ * child_ids / child_visits / child_moves [i][SPAI_CHESS_MAX_MOVES], n_children [i]. */
+int spai_chess_trees_create(spai_chess *e, uint32_t n);                   /* n x Tree::default() */
+int spai_chess_search(spai_chess *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_searches, float *policy,
+                      uint32_t *child_ids, float *child_visits, uint16_t *child_moves, uint32_t *n_children);
+/* Tree::use_subtree for the k-th root child (k in [0, n_children)); the new root keeps N and W */
+int spai_chess_tree_use_subtree(spai_chess *e, uint32_t tree, uint32_t child_index);
+int spai_chess_tree_root(spai_chess *e, uint32_t tree, spai_chess_state *root, uint32_t *visits, float *value_sum);
+
+/* SelfPlayWorker::self_play (learner_concurrent.rs:169-242) for chess */
+typedef void (*spai_chess_sample_sink)(void *user, uint32_t game_id, uint32_t n,
+                                       const float *encodings /* [n][19*64] */,
+                                       const float *policies /* [n][4672] */, const float *values /* [n] */,
+                                       const uint16_t *moves /* [n] move played at each position */);
+int spai_chess_selfplay_run(spai_chess *e, uint32_t n_games, uint64_t game_id_base, spai_chess_sample_sink sink,
+                            void *user, spai_selfplay_stats *stats);
+/* timing of the last search / self-play call, as spai_engine_timing:
+ * ms[0] select + leaf rules, ms[1] net forward, ms[2] expand + backup */
+int spai_chess_set_timing(spai_chess *e, int enabled);
+int spai_chess_timing(spai_chess *e, double *avg_ms, double *launches, double *items);
+
 #ifdef __cplusplus
 }
 #endif

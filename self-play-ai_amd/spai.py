@@ -37,6 +37,14 @@ SYMBOLS = [
     "spai_learner_set_comm", "spai_params_save_safetensors", "spai_params_load_safetensors",
     "spai_replay_create", "spai_replay_destroy", "spai_replay_push", "spai_replay_pop", "spai_replay_size",
     "spai_choose_multiple", "spai_pipeline_config_default", "spai_pipeline_run", "spai_learner_train",
+    # chess (spai_chess.py)
+    "spai_chess_config_default", "spai_chess_create", "spai_chess_destroy", "spai_chess_sync",
+    "spai_chess_games_resize", "spai_chess_games_write", "spai_chess_games_read", "spai_chess_legal_moves",
+    "spai_chess_apply", "spai_chess_status", "spai_chess_encode", "spai_chess_mask_invalid",
+    "spai_chess_move_index", "spai_chess_index_move", "spai_chess_net_num_params", "spai_chess_net_init_params",
+    "spai_chess_net_create", "spai_chess_net_destroy", "spai_chess_net_forward", "spai_chess_set_net",
+    "spai_chess_trees_create", "spai_chess_search", "spai_chess_tree_use_subtree", "spai_chess_tree_root",
+    "spai_chess_selfplay_run", "spai_chess_set_timing", "spai_chess_timing",
 ]
 COMM_ID_BYTES = 128
 
