@@ -374,6 +374,10 @@ int spai_chess_search(spai_chess *e, uint32_t n, const uint32_t *tree_idx, uint3
 /* Tree::use_subtree for the k-th root child (k in [0, n_children)); the new root keeps N and W */
 int spai_chess_tree_use_subtree(spai_chess *e, uint32_t tree, uint32_t child_index);
 int spai_chess_tree_root(spai_chess *e, uint32_t tree, spai_chess_state *root, uint32_t *visits, float *value_sum);
+/* use_subtree for n trees at once (child_index[i] of tree_idx[i]'s root children); status[i] /
+ * reps[i] = get_status / get_num_repetitions of the new root (either may be NULL) */
+int spai_chess_trees_advance(spai_chess *e, uint32_t n, const uint32_t *tree_idx, const uint32_t *child_index,
+                             uint8_t *status, uint32_t *reps);
 
 /* SelfPlayWorker::self_play (learner_concurrent.rs:169-242) for chess */
 typedef void (*spai_chess_sample_sink)(void *user, uint32_t game_id, uint32_t n,

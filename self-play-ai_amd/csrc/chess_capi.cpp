@@ -268,6 +268,14 @@ int spai_chess_tree_root(spai_chess *e, uint32_t tree, spai_chess_state *root, u
     return tree_root(e, tree, root, visits, value_sum);
 }
 
+int spai_chess_trees_advance(spai_chess *e, uint32_t n, const uint32_t *tree_idx, const uint32_t *child_index,
+                             uint8_t *status, uint32_t *reps) {
+    CH_CHECK(e);
+    CH_PTR(tree_idx);
+    CH_PTR(child_index);
+    return trees_advance(e, n, tree_idx, child_index, status, reps);
+}
+
 int spai_chess_selfplay_run(spai_chess *e, uint32_t n_games, uint64_t game_id_base, spai_chess_sample_sink sink,
                             void *user, spai_selfplay_stats *stats) {
     CH_CHECK(e);

@@ -680,6 +680,31 @@ int tree_use_subtree(spai_chess *e, uint32_t tree, uint32_t child_index) {
     return check_err(e);
 }
 
+int trees_advance(spai_chess *e, uint32_t n, const uint32_t *tree_idx, const uint32_t *child_index, uint8_t *status,
+                  uint32_t *reps) {
+    Trees &Tr = e->trees;
+    SPAI_CHECK(n >= 1 && n <= Tr.n, SPAI_ERR_INVALID, "advance: n=%u trees (have %u)", n, Tr.n);
+    for (uint32_t i = 0; i < n; ++i)
+        SPAI_CHECK(tree_idx[i] < Tr.n, SPAI_ERR_INVALID, "tree index %u out of range", tree_idx[i]);
+    SPAI_HIP(hipMemcpyAsync(e->active.p, tree_idx, 4 * n, hipMemcpyHostToDevice, e->stream));
+    SPAI_TRY(root_stats(e, n));
+    for (uint32_t i = 0; i < n; ++i)
+        SPAI_CHECK(child_index[i] < Tr.h_nch[i], SPAI_ERR_INVALID, "tree %u: child index %u >= %u root children",
+                   tree_idx[i], child_index[i], Tr.h_nch[i]);
+    SPAI_HIP(hipMemcpyAsync(Tr.adv_pick.p, child_index, 4 * n, hipMemcpyHostToDevice, e->stream));
+    k_cadvance<<<blocks_for(n), 64 * kWavesPerBlock, 0, e->stream>>>(view(e), e->active.p, n, Tr.adv_pick.p,
+                                                                     Tr.adv_out.p, Tr.adv_board.p, e->err.p);
+    SPAI_HIP(hipGetLastError());
+    std::vector<uint32_t> out(n);
+    SPAI_HIP(hipMemcpyAsync(out.data(), Tr.adv_out.p, 4 * n, hipMemcpyDeviceToHost, e->stream));
+    SPAI_TRY(check_err(e));
+    for (uint32_t i = 0; i < n; ++i) {
+        if (status) status[i] = (uint8_t)(out[i] & 0xFF);
+        if (reps) reps[i] = out[i] >> 8;
+    }
+    return SPAI_OK;
+}
+
 int tree_root(spai_chess *e, uint32_t tree, spai_chess_state *root, uint32_t *visits, float *value_sum) {
     Trees &Tr = e->trees;
     SPAI_CHECK(tree < Tr.n, SPAI_ERR_INVALID, "tree %u out of range", tree);

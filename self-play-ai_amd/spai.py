@@ -43,7 +43,7 @@ SYMBOLS = [
     "spai_chess_apply", "spai_chess_status", "spai_chess_encode", "spai_chess_mask_invalid",
     "spai_chess_move_index", "spai_chess_index_move", "spai_chess_net_num_params", "spai_chess_net_init_params",
     "spai_chess_net_create", "spai_chess_net_destroy", "spai_chess_net_forward", "spai_chess_set_net",
-    "spai_chess_trees_create", "spai_chess_search", "spai_chess_tree_use_subtree", "spai_chess_tree_root",
+    "spai_chess_trees_create", "spai_chess_search", "spai_chess_tree_use_subtree", "spai_chess_tree_root", "spai_chess_trees_advance",
     "spai_chess_selfplay_run", "spai_chess_set_timing", "spai_chess_timing",
 ]
 COMM_ID_BYTES = 128

@@ -57,6 +57,7 @@ def lib():
         L.spai_chess_search.argtypes = [vp, u32, vp, u32, vp, vp, vp, vp, vp]
         L.spai_chess_tree_use_subtree.argtypes = [vp, u32, u32]
         L.spai_chess_tree_root.argtypes = [vp, u32, vp, vp, vp]
+        L.spai_chess_trees_advance.argtypes = [vp, u32, vp, vp, vp, vp]
         L.spai_chess_selfplay_run.argtypes = [vp, u32, u64, SINK, vp, P(SelfPlayStats)]
         L.spai_chess_set_timing.argtypes = [vp, i32]
         L.spai_chess_timing.argtypes = [vp, vp, vp, vp]
@@ -206,6 +207,14 @@ class ChessEngine:
 
     def use_subtree(self, tree, child_index):
         _check(lib().spai_chess_tree_use_subtree(self.h, tree, child_index))
+
+    def advance(self, trees, child_index):
+        t = np.ascontiguousarray(trees, np.uint32)
+        k = np.ascontiguousarray(child_index, np.uint32)
+        st = np.zeros(len(t), np.uint8)
+        reps = np.zeros(len(t), np.uint32)
+        _check(lib().spai_chess_trees_advance(self.h, len(t), _p(t), _p(k), _p(st), _p(reps)))
+        return st, reps
 
     def tree_root(self, tree):
         st = np.zeros(1, STATE_DTYPE)
