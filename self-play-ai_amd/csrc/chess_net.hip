@@ -8,20 +8,21 @@
 // linear 64->256 + ReLU + linear 256->1 + tanh.  BN (eval) folded into the convs.
 //
 // MI355X design:
-//  * one workgroup = 4 waves = 2 positions' whole forward.  Both boards' 128
+//  * one workgroup = 8 waves (two per SIMD) = 2 positions' whole forward.  Both boards' 128
 //    cells x 256 channels stay in LDS for every layer (two bf16 buffers of
 //    64 KiB: layer input and output; the residual is the input buffer, updated
 //    in place), so activations never touch HBM; only weights stream (L2).
 //  * every conv is an implicit GEMM on v_mfma_f32_16x16x32_bf16, D[co][cell] =
-//    W[co][k] X[k][cell], k = tap*256 + ci.  Wave w owns co tiles 4w..4w+3 (64
-//    output channels) over all 8 cell tiles (two boards), so a k-step is 32
-//    MFMAs on 4 weight fragments (global, pre-packed in exact fragment order:
-//    one coalesced 1 KiB load each) and 8 activation fragments (ds_read_b128).
+//    W[co][k] X[k][cell], k = tap*256 + ci.  Wave w owns co tiles 2w, 2w+1 (32
+//    output channels) over all 8 cell tiles (two boards), so a k-step is 16
+//    MFMAs on 2 weight fragments (global, pre-packed in exact fragment order:
+//    one coalesced 1 KiB load each, 3 k-steps ahead) and 8 activation
+//    fragments (ds_read_b128, immediate offsets).
 //    A whole board is inside the workgroup, so a 3x3 tap is a row shift;
 //    off-board taps read a zero row.
-//  * LDS rows are 512 B ([cell][256 ch] bf16) with the 16-B chunk index
-//    XOR-ed by (cell & 7) << 1: for every tap shift the 16 lanes of each
-//    ds_read_b128 lane group hit 16 distinct bank quads.
+//  * LDS rows hold [cell][256 ch] bf16 at a 544-B pitch: for every tap shift the
+//    16 lanes of each ds_read_b128 lane group hit 16 distinct bank quads
+//    (row_chunk), and a k-step's read is the tap's row base + a constant.
 //  * bias is the first MFMA's C operand; epilogues fuse ReLU and the residual.
 // Algorithmic FLOPs per position at 20 blocks: 3,036,348,928.
 #include <algorithm>
@@ -43,15 +44,22 @@ typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kHid = 256;
-constexpr int kWaves = 4;
+#ifndef SPAI_CHESS_WAVES
+#define SPAI_CHESS_WAVES 8
+#endif
+constexpr int kWaves = SPAI_CHESS_WAVES;     // 4: one wave per SIMD; 8: two
+constexpr int kCPW = 16 / kWaves;             // co tiles (of 16 channels) per wave
+constexpr int kTPW = 8 / kWaves;              // policy-output cell tiles per wave
 constexpr int kThreads = 64 * kWaves;
 constexpr int kPos = 2;                       // positions per workgroup
 constexpr int kRows = kPos * 64;              // LDS rows (cells)
-constexpr int kRowB = kHid * 2;               // 512 B per row
+constexpr int kRowB = kHid * 2;               // 512 B of channels per row
+constexpr int kStride = kRowB + 32;           // 544 B row pitch (see row_chunk)
 constexpr int kBufA = 0;
-constexpr int kBufB = kRows * kRowB;          // 65536
-constexpr int kZero = 2 * kRows * kRowB;      // 131072: one zero row
-constexpr int kSmem = kZero + kRowB;          // 131584 B
+constexpr int kBufB = kRows * kStride;        // 69632
+constexpr int kZero = 2 * kRows * kStride;    // 139264: zeros for off-board taps
+constexpr int kZeroB = 768;
+constexpr int kSmem = kZero + kZeroB;         // 140032 B
 constexpr int kCT = kHid / 16;                // 16 co tiles
 constexpr int kPolCT = 5;                     // 73 policy channels -> 80
 constexpr int kFrag = 64;                     // uint4 per fragment (1 KiB)
@@ -72,25 +80,43 @@ __device__ __forceinline__ uint32_t pack_relu_bf16x2(float a, float b) {
 __device__ __forceinline__ float bf_lo(uint32_t u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf_hi(uint32_t u) { return __uint_as_float(u & 0xFFFF0000u); }
 
-// byte offset of 16-B chunk `c` of row `v` inside a buffer
-__device__ __forceinline__ int row_chunk(int v, int c) { return v * kRowB + ((c ^ ((v & 7) << 1)) << 4); }
+// byte offset of 16-B chunk `c` (channels 8c..8c+7) of row `v` inside a buffer.
+// The 544-B pitch puts row v's chunk c in bank quad (2v + c) mod 16: the 16 lanes
+// of a ds_read_b128 lane group (two k-groups q of opposite parity, 8 consecutive
+// rows each, for any tap shift) land in 16 distinct bank quads, and a k-step's
+// address is the tap's row base plus a compile-time offset.
+__device__ __forceinline__ int row_chunk(int v, int c) { return v * kStride + (c << 4); }
 
 // Implicit-GEMM conv over the LDS buffer at IN: TAPS (9 = 3x3 pad 1, 1 = 1x1)
 // x CB channel blocks of 32.  acc[c][t]: co tile 4*wave + c, cell tile t.
+// Software pipeline (fully unrolled, so every ring slot is static): weight
+// fragments (global/L2) DA-1 k-steps ahead, activation fragments (LDS) one
+// k-step ahead; the first k-step takes the bias as its C operand.
+#ifndef SPAI_CHESS_DA
+#define SPAI_CHESS_DA 4   // weight ring: 3 k-steps ahead (measured: 2 -> 3.40 ms, 8 -> 2.19 ms at 4 waves)
+#endif
+#ifndef SPAI_CHESS_DB
+#define SPAI_CHESS_DB 2
+#endif
+#ifndef SPAI_CHESS_SCHED
+#define SPAI_CHESS_SCHED 0
+#endif
 template <int TAPS, int CB>
 __device__ __forceinline__ void conv(const uint8_t *smem, int in, const uint4 *__restrict__ w,
-                                     const float *__restrict__ bias, int wave, int lane, f32x4 (&acc)[4][8]) {
+                                     const float *__restrict__ bias, int wave, int lane, f32x4 (&acc)[kCPW][8]) {
+    constexpr int DA = SPAI_CHESS_DA;
     const int q = lane >> 4, col = lane & 15;
+    f32x4 bv[kCPW];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        const float4 b = *(const float4 *)(bias + (4 * wave + c) * 16 + 4 * q);
-#pragma unroll
-        for (int t = 0; t < 8; ++t) acc[c][t] = f32x4{b.x, b.y, b.z, b.w};
+    for (int c = 0; c < kCPW; ++c) {
+        const float4 b = *(const float4 *)(bias + (kCPW * wave + c) * 16 + 4 * q);
+        bv[c] = f32x4{b.x, b.y, b.z, b.w};
     }
-    const uint4 *wl = w + (size_t)(4 * wave) * kFrag + lane;
+    const uint4 *wl = w + (size_t)(kCPW * wave) * kFrag + lane;
     constexpr int KS = TAPS * CB;
-    uint4 A[2][4], B[2][8];
-    int rowoff[8], swz[8];
+    constexpr int DB = (CB % SPAI_CHESS_DB == 0) ? SPAI_CHESS_DB : 2;
+    uint4 A[DA][kCPW], B[DB > 2 ? DB : 2][8];
+    int rowoff[8];
     auto geo = [&](int tap) {
         const int dy = TAPS == 9 ? tap / 3 - 1 : 0, dx = TAPS == 9 ? tap % 3 - 1 : 0;
 #pragma unroll
@@ -99,54 +125,91 @@ __device__ __forceinline__ void conv(const uint8_t *smem, int in, const uint4 *_
             const int y = (cell >> 3) + dy, x = (cell & 7) + dx;
             const int v = (t >> 2) * 64 + y * 8 + x;
             const bool ok = (unsigned)y < 8u && (unsigned)x < 8u;
-            rowoff[t] = ok ? in + v * kRowB : kZero;
-            swz[t] = (v & 7) << 1;
+            // an off-board tap reads zeros in the bank quad its row would use
+            rowoff[t] = (ok ? in + v * kStride : kZero + ((v & 7) << 5)) + (q << 4);
         }
     };
-    auto load = [&](int ks, uint4 (&a)[4], uint4 (&b)[8]) {
+    auto load_a = [&](int ks, uint4 (&a)[kCPW]) {
+#pragma unroll
+        for (int c = 0; c < kCPW; ++c) a[c] = wl[((size_t)ks * kCT + c) * kFrag];
+    };
+    auto load_b = [&](int ks, uint4 (&b)[8]) {
         const int cb = ks % CB;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) a[c] = wl[((size_t)ks * kCT + c) * kFrag];
-#pragma unroll
-        for (int t = 0; t < 8; ++t) b[t] = *(const uint4 *)(smem + rowoff[t] + ((((4 * cb + q) ^ swz[t])) << 4));
+        for (int t = 0; t < 8; ++t) b[t] = *(const uint4 *)(smem + rowoff[t] + (cb << 6));
     };
+#pragma unroll
+    for (int c = 0; c < kCPW; ++c)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[c][t] = bv[c];
+#pragma unroll
+    for (int k = 0; k < DA - 1; ++k)
+        if (k < KS) load_a(k, A[k]);
     geo(0);
-    load(0, A[0], B[0]);
-    for (int ks = 0; ks < KS; ks += 2) {
-        if (ks + 1 < KS) {
-            if ((ks + 1) % CB == 0) geo((ks + 1) / CB);
-            load(ks + 1, A[1], B[1]);
+    if constexpr (CB % DA == 0 && CB % DB == 0) {
+        // taps as a runtime loop, channel blocks unrolled: ring slots stay static
+#pragma unroll
+        for (int k = 0; k < DB - 1; ++k) load_b(k, B[k]);
+        for (int tap = 0; tap < TAPS; ++tap) {
+#pragma unroll
+            for (int cb = 0; cb < CB; ++cb) {
+                const int ks = tap * CB + cb;
+                if (ks + DA - 1 < KS) load_a(ks + DA - 1, A[(cb + DA - 1) % DA]);
+                const int kb = cb + DB - 1;   // next activation k-step to fetch
+                if (kb < CB) {
+                    load_b(kb, B[kb % DB]);
+                } else if (tap + 1 < TAPS) {
+                    if (kb == CB) geo(tap + 1);   // every fetch of this tap is already issued
+                    load_b(kb - CB, B[kb % DB]);
+                }
+#pragma unroll
+                for (int c = 0; c < kCPW; ++c)
+#pragma unroll
+                    for (int t = 0; t < 8; ++t)
+                        acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[cb % DA][c]),
+                                                                            as_bf16x8(B[cb % DB][t]), acc[c][t], 0, 0, 0);
+#if SPAI_CHESS_SCHED
+                // issue order: each MFMA followed by up to one LDS read, one weight load, two VALU
+#pragma unroll
+                for (int i = 0; i < kCPW * 8; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    if (i < 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    if (i < 4) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#endif
+            }
         }
+    } else {
+        load_b(0, B[0]);
 #pragma unroll
-        for (int c = 0; c < 4; ++c)
+        for (int ks = 0; ks < KS; ++ks) {
+            if (ks + DA - 1 < KS) load_a(ks + DA - 1, A[(ks + DA - 1) % DA]);
+            if (ks + 1 < KS) {
+                if ((ks + 1) % CB == 0) geo((ks + 1) / CB);
+                load_b(ks + 1, B[(ks + 1) & 1]);
+            }
 #pragma unroll
-            for (int t = 0; t < 8; ++t)
-                acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[0][c]), as_bf16x8(B[0][t]), acc[c][t],
-                                                                    0, 0, 0);
-        if (ks + 1 >= KS) break;
-        if (ks + 2 < KS) {
-            if ((ks + 2) % CB == 0) geo((ks + 2) / CB);
-            load(ks + 2, A[0], B[0]);
+            for (int c = 0; c < kCPW; ++c)
+#pragma unroll
+                for (int t = 0; t < 8; ++t)
+                    acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[ks % DA][c]),
+                                                                        as_bf16x8(B[ks & 1][t]), acc[c][t], 0, 0, 0);
         }
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-#pragma unroll
-            for (int t = 0; t < 8; ++t)
-                acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[1][c]), as_bf16x8(B[1][t]), acc[c][t],
-                                                                    0, 0, 0);
     }
 }
 
 // relu(acc [+ residual at OUT]) -> bf16 at OUT (in place over the residual)
 template <bool RES>
-__device__ __forceinline__ void epilogue(uint8_t *smem, int out, int wave, int lane, const f32x4 (&acc)[4][8]) {
+__device__ __forceinline__ void epilogue(uint8_t *smem, int out, int wave, int lane, const f32x4 (&acc)[kCPW][8]) {
     const int q = lane >> 4, col = lane & 15;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+    for (int c = 0; c < kCPW; ++c)
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
             const int v = (t >> 2) * 64 + (t & 3) * 16 + col;
-            const int chunk = (4 * wave + c) * 2 + (q >> 1);
+            const int chunk = (kCPW * wave + c) * 2 + (q >> 1);
             uint2 *p = (uint2 *)(smem + out + row_chunk(v, chunk) + (q & 1) * 8);
             f32x4 a = acc[c][t];
             if (RES) {
@@ -177,9 +240,9 @@ __global__ void __launch_bounds__(kThreads, 1)
         if (slot < count) d = *(const uint4 *)(x + ((size_t)slot * 64 + (v & 63)) * kInCh + c * 8);
         *(uint4 *)(smem + kBufB + row_chunk(v, c)) = d;
     }
-    for (int i = tid; i < kRowB / 16; i += kThreads) *(uint4 *)(smem + kZero + i * 16) = make_uint4(0, 0, 0, 0);
+    for (int i = tid; i < kZeroB / 16; i += kThreads) *(uint4 *)(smem + kZero + i * 16) = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    f32x4 acc[4][8];
+    f32x4 acc[kCPW][8];
     conv<9, 1>(smem, kBufB, W.w_stem, W.b_stem, wave, lane, acc);
     epilogue<false>(smem, kBufA, wave, lane, acc);
     __syncthreads();
@@ -199,45 +262,38 @@ __global__ void __launch_bounds__(kThreads, 1)
     __syncthreads();
     {
         // conv1x1 256->256 output in B; torso output still in A.  Value conv
-        // over A: 2 threads per cell, 128 channels each.
-        const int v = tid >> 1, half = tid & 1;
+        // over A: TPC threads per cell, 256/TPC channels each.
+        constexpr int TPC = kThreads / kRows, CPT = 32 / TPC;
+        const int v = tid / TPC, part = tid % TPC;
         float s = 0.f;
 #pragma unroll 4
-        for (int k = 0; k < 16; ++k) {
-            const int c = half * 16 + k;
+        for (int k = 0; k < CPT; ++k) {
+            const int c = part * CPT + k;
             const uint4 d = *(const uint4 *)(smem + kBufA + row_chunk(v, c));
             const float4 w0 = *(const float4 *)(W.v_w + c * 8), w1 = *(const float4 *)(W.v_w + c * 8 + 4);
             s += bf_lo(d.x) * w0.x + bf_hi(d.x) * w0.y + bf_lo(d.y) * w0.z + bf_hi(d.y) * w0.w;
             s += bf_lo(d.z) * w1.x + bf_hi(d.z) * w1.y + bf_lo(d.w) * w1.z + bf_hi(d.w) * w1.w;
         }
-        s += __shfl_xor(s, 1, 64);
+#pragma unroll
+        for (int o = 1; o < TPC; o <<= 1) s += __shfl_xor(s, o, 64);
         __syncthreads();   // every wave is done reading A (conv1x1 above, value conv here)
         float *vcell = (float *)(smem + kBufA);           // [128] value-conv features
         float *hid = (float *)(smem + kBufA + 1024);      // [2][256]
         float *red = (float *)(smem + kBufA + 4096);      // [2][4] wave partials
-        if (half == 0) vcell[v] = fmaxf(s + W.v_b[0], 0.f);
+        if (part == 0) vcell[v] = fmaxf(s + W.v_b[0], 0.f);
         __syncthreads();
         {
-            const int j = tid;   // linear 64 -> 256 + ReLU, both positions
+            const int j = tid & 255;   // linear 64 -> 256 + ReLU, then the 256 -> 1 partial
             const float *wr = W.l1_w + (size_t)j * 64;
-            float h0 = W.l1_b[j], h1 = h0;
-            for (int c = 0; c < 64; ++c) {
-                const float wv = wr[c];
-                h0 += wv * vcell[c];
-                h1 += wv * vcell[64 + c];
-            }
-            hid[j] = fmaxf(h0, 0.f);
-            hid[256 + j] = fmaxf(h1, 0.f);
-            // linear 256 -> 1: block reduction
-            float p0 = W.l2_w[j] * hid[j], p1 = W.l2_w[j] * hid[256 + j];
+            for (int sp = tid >> 8; sp < kPos; sp += kThreads / 256) {
+                float h = W.l1_b[j];
+                for (int c = 0; c < 64; ++c) h += wr[c] * vcell[sp * 64 + c];
+                h = fmaxf(h, 0.f);
+                hid[sp * 256 + j] = h;
+                float pr = W.l2_w[j] * h;
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) {
-                p0 += __shfl_xor(p0, o, 64);
-                p1 += __shfl_xor(p1, o, 64);
-            }
-            if (lane == 0) {
-                red[wave] = p0;
-                red[4 + wave] = p1;
+                for (int o = 32; o > 0; o >>= 1) pr += __shfl_xor(pr, o, 64);
+                if (lane == 0) red[sp * 4 + (j >> 6)] = pr;
             }
         }
         __syncthreads();
@@ -250,33 +306,34 @@ __global__ void __launch_bounds__(kThreads, 1)
     // ---- policy conv1x1 256->73 over B -> logits [slot][ch*64 + cell]
     {
         const int q = lane >> 4, col = lane & 15;
-        f32x4 pa[kPolCT][2];
+        f32x4 pa[kPolCT][kTPW];
 #pragma unroll
         for (int c = 0; c < kPolCT; ++c) {
             const float4 b = *(const float4 *)(W.b_p2 + c * 16 + 4 * q);
-            pa[c][0] = pa[c][1] = f32x4{b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int u = 0; u < kTPW; ++u) pa[c][u] = f32x4{b.x, b.y, b.z, b.w};
         }
 #pragma unroll 2
         for (int ks = 0; ks < 8; ++ks) {
-            uint4 a[kPolCT], b[2];
+            uint4 a[kPolCT], b[kTPW];
 #pragma unroll
             for (int c = 0; c < kPolCT; ++c) a[c] = W.w_p2[((size_t)ks * kPolCT + c) * kFrag + lane];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int t = 2 * wave + u;
+            for (int u = 0; u < kTPW; ++u) {
+                const int t = kTPW * wave + u;
                 const int v = (t >> 2) * 64 + (t & 3) * 16 + col;
                 b[u] = *(const uint4 *)(smem + kBufB + row_chunk(v, 4 * ks + q));
             }
 #pragma unroll
             for (int c = 0; c < kPolCT; ++c)
 #pragma unroll
-                for (int u = 0; u < 2; ++u)
+                for (int u = 0; u < kTPW; ++u)
                     pa[c][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[c]), as_bf16x8(b[u]), pa[c][u], 0,
                                                                        0, 0);
         }
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int t = 2 * wave + u;
+        for (int u = 0; u < kTPW; ++u) {
+            const int t = kTPW * wave + u;
             const uint32_t slot = slot0 + (t >> 2);
             const int cell = (t & 3) * 16 + col;
             if (slot < count) {
