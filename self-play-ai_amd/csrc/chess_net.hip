@@ -8,16 +8,17 @@
 // linear 64->256 + ReLU + linear 256->1 + tanh.  BN (eval) folded into the convs.
 //
 // MI355X design:
-//  * one workgroup = 8 waves (two per SIMD) = 2 positions' whole forward.  Both boards' 128
+//  * one workgroup = 4 waves (one per SIMD) = 2 positions' whole forward.  Both boards' 128
 //    cells x 256 channels stay in LDS for every layer (two bf16 buffers of
 //    64 KiB: layer input and output; the residual is the input buffer, updated
 //    in place), so activations never touch HBM; only weights stream (L2).
 //  * every conv is an implicit GEMM on v_mfma_f32_16x16x32_bf16, D[co][cell] =
-//    W[co][k] X[k][cell], k = tap*256 + ci.  Wave w owns co tiles 2w, 2w+1 (32
-//    output channels) over all 8 cell tiles (two boards), so a k-step is 16
-//    MFMAs on 2 weight fragments (global, pre-packed in exact fragment order:
-//    one coalesced 1 KiB load each, 3 k-steps ahead) and 8 activation
-//    fragments (ds_read_b128, immediate offsets).
+//    W[co][k] X[k][cell], k = tap*256 + ci.  Wave w owns co tiles 4w..4w+3 (64
+//    output channels) over all 8 cell tiles (two boards), so a k-step is 32
+//    MFMAs on 4 weight fragments (global, pre-packed in exact fragment order:
+//    one coalesced 1 KiB load each, issued 3 k-steps ahead and pinned there by
+//    a scheduling barrier) and 8 activation fragments (ds_read_b128, immediate
+//    offsets).
 //    A whole board is inside the workgroup, so a 3x3 tap is a row shift;
 //    off-board taps read a zero row.
 //  * LDS rows hold [cell][256 ch] bf16 at a 544-B pitch: for every tap shift the
@@ -45,7 +46,7 @@ typedef short i16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int kHid = 256;
 #ifndef SPAI_CHESS_WAVES
-#define SPAI_CHESS_WAVES 8
+#define SPAI_CHESS_WAVES 4   // 8 (two per SIMD) measured equal: 2.101 vs 2.101 ms
 #endif
 constexpr int kWaves = SPAI_CHESS_WAVES;     // 4: one wave per SIMD; 8: two
 constexpr int kCPW = 16 / kWaves;             // co tiles (of 16 channels) per wave
@@ -100,6 +101,9 @@ __device__ __forceinline__ int row_chunk(int v, int c) { return v * kStride + (c
 #endif
 #ifndef SPAI_CHESS_SCHED
 #define SPAI_CHESS_SCHED 0
+#endif
+#ifndef SPAI_CHESS_PIN
+#define SPAI_CHESS_PIN 1
 #endif
 template <int TAPS, int CB>
 __device__ __forceinline__ void conv(const uint8_t *smem, int in, const uint4 *__restrict__ w,
@@ -162,6 +166,11 @@ __device__ __forceinline__ void conv(const uint8_t *smem, int in, const uint4 *_
                     if (kb == CB) geo(tap + 1);   // every fetch of this tap is already issued
                     load_b(kb - CB, B[kb % DB]);
                 }
+#if SPAI_CHESS_PIN
+                // keep the prefetches here: the scheduler would otherwise sink them
+                // next to their MFMAs and expose the full L2 latency every k-step
+                __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
                 for (int c = 0; c < kCPW; ++c)
 #pragma unroll
