@@ -391,6 +391,45 @@ int spai_chess_selfplay_run(spai_chess *e, uint32_t n_games, uint64_t game_id_ba
 int spai_chess_set_timing(spai_chess *e, int enabled);
 int spai_chess_timing(spai_chess *e, double *avg_ms, double *launches, double *items);
 
+
+/* ---------------------------------------------------------------- tictactoe
+ * game/tictactoe.rs + model/tictactoe.rs (BASELINE config 1) on the device.
+ * Board = two 9-bit masks, bit row*3 + col (the flat action index of the
+ * row-major 3x3 Policy, tictactoe.rs:100-102); X moves first; X to move iff
+ * num_actions_played is even.  Same conventions as the Connect4 entry points;
+ * the net is fp32 (hidden 64) and the policy has 9 entries. */
+typedef struct spai_ttt_state {
+    uint16_t x, o;
+    uint8_t num_actions_played, status;
+    uint8_t pad[2];
+} spai_ttt_state;
+typedef struct spai_ttt spai_ttt;
+typedef struct spai_ttt_net spai_ttt_net;
+int spai_ttt_create(const spai_config *cfg, int device, spai_ttt **out);
+int spai_ttt_destroy(spai_ttt *e);
+int spai_ttt_games_resize(spai_ttt *e, uint32_t n);
+int spai_ttt_games_write(spai_ttt *e, uint32_t first, uint32_t n, const spai_ttt_state *s);
+int spai_ttt_games_read(spai_ttt *e, uint32_t first, uint32_t n, spai_ttt_state *s);
+int spai_ttt_legal_mask(spai_ttt *e, uint32_t first, uint32_t n, uint32_t *mask);        /* tictactoe.rs:169-182 */
+int spai_ttt_apply(spai_ttt *e, uint32_t first, uint32_t n, const int32_t *actions, int32_t *rc);  /* :127-167 */
+int spai_ttt_encode(spai_ttt *e, uint32_t first, uint32_t n, float *out);                /* [n][3][3][3], :199-216 */
+int spai_ttt_mask_invalid(spai_ttt *e, uint32_t first, uint32_t n, const float *policy, uint32_t len,
+                          float *out);                                                   /* :218-236, len 9 */
+int spai_ttt_net_num_params(int blocks, size_t *count);
+int spai_ttt_net_init_params(int blocks, uint64_t seed, float *params);
+int spai_ttt_net_create(spai_ttt *e, int blocks, const float *params, size_t n_params, spai_ttt_net **out);
+int spai_ttt_net_destroy(spai_ttt_net *net);
+int spai_ttt_net_forward(spai_ttt_net *net, uint32_t n, const float *x, float *logits, float *value);
+int spai_ttt_set_net(spai_ttt *e, spai_ttt_net *net);
+int spai_ttt_trees_create(spai_ttt *e, uint32_t n);
+/* per tree i: policy [i][9], child_ids / child_visits [i][9], n_children [i] (any may be NULL) */
+int spai_ttt_search(spai_ttt *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_searches, float *policy,
+                    uint32_t *child_ids, float *child_visits, uint32_t *n_children);
+int spai_ttt_tree_use_subtree(spai_ttt *e, uint32_t tree, uint32_t child_index);
+/* SelfPlayWorker::self_play; the sink gets encodings [n][27], policies [n][9], values, moves */
+int spai_ttt_selfplay_run(spai_ttt *e, uint32_t n_games, uint64_t game_id_base, spai_sample_sink sink, void *user,
+                          spai_selfplay_stats *stats);
+
 #ifdef __cplusplus
 }
 #endif
