@@ -350,6 +350,7 @@ int spai_engine_set_timing(spai_engine *e, int enabled) {
     ENG_CHECK(e);
     KernelTimer &K = e->timer;
     K.enabled = enabled != 0;
+    K.stride = enabled > 1 ? (uint32_t)enabled : 4u;
     for (int i = 0; i < 3; ++i) K.total_ms[i] = K.launches[i] = K.items[i] = 0;
     K.used = 0;
     K.which.clear();

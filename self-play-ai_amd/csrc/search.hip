@@ -425,7 +425,7 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
             const BatchView bv = batch_view(e, h, cur);
             const uint32_t nh = cnt[h], g8 = (nh + kTreesPerBlock - 1) / kTreesPerBlock;
             const uint32_t *act = e->active.p + off[h];
-            const bool sample = timed && h == 0 && (it % 4 == 0);
+            const bool sample = timed && h == 0 && (it % e->timer.stride == 0);
             if (sample) SPAI_TRY(timer_record(e, 0, it, true));
             k_select<<<g8, kBlock, 0, sh>>>(tv, bv, act, nh, e->cfg.c, e->err.p);
             if (sample) SPAI_TRY(timer_record(e, 0, it, false));

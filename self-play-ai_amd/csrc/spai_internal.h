@@ -101,6 +101,7 @@ struct Batch {
 
 struct KernelTimer {
     bool enabled = false;
+    uint32_t stride = 4;            // sample every stride-th search iteration
     double total_ms[3] = {0, 0, 0};
     double launches[3] = {0, 0, 0};
     double items[3] = {0, 0, 0};

@@ -384,8 +384,9 @@ class Engine:
         return games, {k: getattr(st, k) for k, _ in SelfPlayStats._fields_}
 
     # ---- profiling
-    def set_timing(self, on):
-        _check(lib().spai_engine_set_timing(self.h, int(bool(on))))
+    def set_timing(self, on, stride=None):
+        """on: enable the sampled HIP events; stride: sample every stride-th iteration (default 4)"""
+        _check(lib().spai_engine_set_timing(self.h, (int(stride) if stride and stride > 1 else 1) if on else 0))
 
     def timing(self):
         avg = np.zeros(3, np.float64)
