@@ -50,7 +50,6 @@ constexpr int kHid = 256;
 #endif
 constexpr int kWaves = SPAI_CHESS_WAVES;     // 4: one wave per SIMD; 8: two
 constexpr int kCPW = 16 / kWaves;             // co tiles (of 16 channels) per wave
-constexpr int kTPW = 8 / kWaves;              // policy-output cell tiles per wave
 constexpr int kThreads = 64 * kWaves;
 constexpr int kPos = 2;                       // positions per workgroup
 constexpr int kRows = kPos * 64;              // LDS rows (cells)
@@ -105,9 +104,9 @@ __device__ __forceinline__ int row_chunk(int v, int c) { return v * kStride + (c
 #ifndef SPAI_CHESS_PIN
 #define SPAI_CHESS_PIN 1
 #endif
-template <int TAPS, int CB>
+template <int TAPS, int CB, int NT>
 __device__ __forceinline__ void conv(const uint8_t *smem, int in, const uint4 *__restrict__ w,
-                                     const float *__restrict__ bias, int wave, int lane, f32x4 (&acc)[kCPW][8]) {
+                                     const float *__restrict__ bias, int wave, int lane, f32x4 (&acc)[kCPW][NT]) {
     constexpr int DA = SPAI_CHESS_DA;
     const int q = lane >> 4, col = lane & 15;
     f32x4 bv[kCPW];
@@ -119,12 +118,12 @@ __device__ __forceinline__ void conv(const uint8_t *smem, int in, const uint4 *_
     const uint4 *wl = w + (size_t)(kCPW * wave) * kFrag + lane;
     constexpr int KS = TAPS * CB;
     constexpr int DB = (CB % SPAI_CHESS_DB == 0) ? SPAI_CHESS_DB : 2;
-    uint4 A[DA][kCPW], B[DB > 2 ? DB : 2][8];
-    int rowoff[8];
+    uint4 A[DA][kCPW], B[DB > 2 ? DB : 2][NT];
+    int rowoff[NT];
     auto geo = [&](int tap) {
         const int dy = TAPS == 9 ? tap / 3 - 1 : 0, dx = TAPS == 9 ? tap % 3 - 1 : 0;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
+        for (int t = 0; t < NT; ++t) {
             const int cell = (t & 3) * 16 + col;
             const int y = (cell >> 3) + dy, x = (cell & 7) + dx;
             const int v = (t >> 2) * 64 + y * 8 + x;
@@ -137,15 +136,15 @@ __device__ __forceinline__ void conv(const uint8_t *smem, int in, const uint4 *_
 #pragma unroll
         for (int c = 0; c < kCPW; ++c) a[c] = wl[((size_t)ks * kCT + c) * kFrag];
     };
-    auto load_b = [&](int ks, uint4 (&b)[8]) {
+    auto load_b = [&](int ks, uint4 (&b)[NT]) {
         const int cb = ks % CB;
 #pragma unroll
-        for (int t = 0; t < 8; ++t) b[t] = *(const uint4 *)(smem + rowoff[t] + (cb << 6));
+        for (int t = 0; t < NT; ++t) b[t] = *(const uint4 *)(smem + rowoff[t] + (cb << 6));
     };
 #pragma unroll
     for (int c = 0; c < kCPW; ++c)
 #pragma unroll
-        for (int t = 0; t < 8; ++t) acc[c][t] = bv[c];
+        for (int t = 0; t < NT; ++t) acc[c][t] = bv[c];
 #pragma unroll
     for (int k = 0; k < DA - 1; ++k)
         if (k < KS) load_a(k, A[k]);
@@ -174,7 +173,7 @@ __device__ __forceinline__ void conv(const uint8_t *smem, int in, const uint4 *_
 #pragma unroll
                 for (int c = 0; c < kCPW; ++c)
 #pragma unroll
-                    for (int t = 0; t < 8; ++t)
+                    for (int t = 0; t < NT; ++t)
                         acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[cb % DA][c]),
                                                                             as_bf16x8(B[cb % DB][t]), acc[c][t], 0, 0, 0);
 #if SPAI_CHESS_SCHED
@@ -202,7 +201,7 @@ __device__ __forceinline__ void conv(const uint8_t *smem, int in, const uint4 *_
 #pragma unroll
             for (int c = 0; c < kCPW; ++c)
 #pragma unroll
-                for (int t = 0; t < 8; ++t)
+                for (int t = 0; t < NT; ++t)
                     acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[ks % DA][c]),
                                                                         as_bf16x8(B[ks & 1][t]), acc[c][t], 0, 0, 0);
         }
@@ -210,13 +209,13 @@ __device__ __forceinline__ void conv(const uint8_t *smem, int in, const uint4 *_
 }
 
 // relu(acc [+ residual at OUT]) -> bf16 at OUT (in place over the residual)
-template <bool RES>
-__device__ __forceinline__ void epilogue(uint8_t *smem, int out, int wave, int lane, const f32x4 (&acc)[kCPW][8]) {
+template <bool RES, int NT>
+__device__ __forceinline__ void epilogue(uint8_t *smem, int out, int wave, int lane, const f32x4 (&acc)[kCPW][NT]) {
     const int q = lane >> 4, col = lane & 15;
 #pragma unroll
     for (int c = 0; c < kCPW; ++c)
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
+        for (int t = 0; t < NT; ++t) {
             const int v = (t >> 2) * 64 + (t & 3) * 16 + col;
             const int chunk = (kCPW * wave + c) * 2 + (q >> 1);
             uint2 *p = (uint2 *)(smem + out + row_chunk(v, chunk) + (q & 1) * 8);
@@ -232,17 +231,14 @@ __device__ __forceinline__ void epilogue(uint8_t *smem, int out, int wave, int l
         }
 }
 
-__global__ void __launch_bounds__(kThreads, 1)
-    k_chess_forward(const uint32_t *__restrict__ d_count, uint32_t max_n, const uint16_t *__restrict__ x, NetW W,
-                    float *__restrict__ logits, float *__restrict__ value) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kSmem];
-    const uint32_t count = d_count ? min(*d_count, max_n) : max_n;
-    const uint32_t slot0 = blockIdx.x * kPos;
-    if (slot0 >= count) return;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+// the forward of P positions (slots slot0 .. slot0+P-1) by one workgroup
+template <int P>
+__device__ __forceinline__ void forward_body(uint8_t *smem, uint32_t count, uint32_t slot0,
+                                             const uint16_t *__restrict__ x, const NetW &W, float *__restrict__ logits,
+                                             float *__restrict__ value, int tid, int lane, int wave) {
+    constexpr int NT = 4 * P, ROWS = 64 * P, TPW = NT / kWaves;
     // stage the input planes (bf16 [cell][32]) into buffer B, chunks 0..3 of each row; zero row
-    for (int i = tid; i < kRows * 4; i += kThreads) {
+    for (int i = tid; i < ROWS * 4; i += kThreads) {
         const int v = i >> 2, c = i & 3;
         const uint32_t slot = slot0 + (v >> 6);
         uint4 d = make_uint4(0, 0, 0, 0);
@@ -251,32 +247,34 @@ __global__ void __launch_bounds__(kThreads, 1)
     }
     for (int i = tid; i < kZeroB / 16; i += kThreads) *(uint4 *)(smem + kZero + i * 16) = make_uint4(0, 0, 0, 0);
     __syncthreads();
-    f32x4 acc[kCPW][8];
-    conv<9, 1>(smem, kBufB, W.w_stem, W.b_stem, wave, lane, acc);
-    epilogue<false>(smem, kBufA, wave, lane, acc);
+    f32x4 acc[kCPW][NT];
+    conv<9, 1, NT>(smem, kBufB, W.w_stem, W.b_stem, wave, lane, acc);
+    epilogue<false, NT>(smem, kBufA, wave, lane, acc);
     __syncthreads();
     for (int l = 0; l < W.blocks; ++l) {
         const size_t l1 = 2 * l, l2 = 2 * l + 1;
-        conv<9, 8>(smem, kBufA, W.w_res + l1 * 72 * kCT * kFrag, W.b_res + l1 * kHid, wave, lane, acc);
-        epilogue<false>(smem, kBufB, wave, lane, acc);
+        conv<9, 8, NT>(smem, kBufA, W.w_res + l1 * 72 * kCT * kFrag, W.b_res + l1 * kHid, wave, lane, acc);
+        epilogue<false, NT>(smem, kBufB, wave, lane, acc);
         __syncthreads();
-        conv<9, 8>(smem, kBufB, W.w_res + l2 * 72 * kCT * kFrag, W.b_res + l2 * kHid, wave, lane, acc);
-        epilogue<true>(smem, kBufA, wave, lane, acc);
+        conv<9, 8, NT>(smem, kBufB, W.w_res + l2 * 72 * kCT * kFrag, W.b_res + l2 * kHid, wave, lane, acc);
+        epilogue<true, NT>(smem, kBufA, wave, lane, acc);
         __syncthreads();
     }
     // ---- policy head: conv1x1 256->256 + ReLU -> buffer B
-    conv<1, 8>(smem, kBufA, W.w_p1, W.b_p1, wave, lane, acc);
-    epilogue<false>(smem, kBufB, wave, lane, acc);
+    conv<1, 8, NT>(smem, kBufA, W.w_p1, W.b_p1, wave, lane, acc);
+    epilogue<false, NT>(smem, kBufB, wave, lane, acc);
     // ---- value head (VALU, fp32): conv1x1 256->1 + ReLU per cell, from buffer A
     __syncthreads();
     {
         // conv1x1 256->256 output in B; torso output still in A.  Value conv
-        // over A: TPC threads per cell, 256/TPC channels each.
-        constexpr int TPC = kThreads / kRows, CPT = 32 / TPC;
+        // over A: 2 threads per cell, 128 channels each (the same reduction
+        // order whatever P is, so a position's value never depends on its batch).
+        constexpr int TPC = 2, CPT = 32 / TPC;
         const int v = tid / TPC, part = tid % TPC;
         float s = 0.f;
 #pragma unroll 4
         for (int k = 0; k < CPT; ++k) {
+            if (v >= ROWS) break;
             const int c = part * CPT + k;
             const uint4 d = *(const uint4 *)(smem + kBufA + row_chunk(v, c));
             const float4 w0 = *(const float4 *)(W.v_w + c * 8), w1 = *(const float4 *)(W.v_w + c * 8 + 4);
@@ -289,12 +287,12 @@ __global__ void __launch_bounds__(kThreads, 1)
         float *vcell = (float *)(smem + kBufA);           // [128] value-conv features
         float *hid = (float *)(smem + kBufA + 1024);      // [2][256]
         float *red = (float *)(smem + kBufA + 4096);      // [2][4] wave partials
-        if (part == 0) vcell[v] = fmaxf(s + W.v_b[0], 0.f);
+        if (part == 0 && v < ROWS) vcell[v] = fmaxf(s + W.v_b[0], 0.f);
         __syncthreads();
         {
             const int j = tid & 255;   // linear 64 -> 256 + ReLU, then the 256 -> 1 partial
             const float *wr = W.l1_w + (size_t)j * 64;
-            for (int sp = tid >> 8; sp < kPos; sp += kThreads / 256) {
+            for (int sp = tid >> 8; sp < P; sp += kThreads / 256) {
                 float h = W.l1_b[j];
                 for (int c = 0; c < 64; ++c) h += wr[c] * vcell[sp * 64 + c];
                 h = fmaxf(h, 0.f);
@@ -306,7 +304,7 @@ __global__ void __launch_bounds__(kThreads, 1)
             }
         }
         __syncthreads();
-        if (tid < kPos) {
+        if (tid < P) {
             const uint32_t slot = slot0 + tid;
             const float *r = red + 4 * tid;
             if (slot < count) value[slot] = tanhf(W.l2_b[0] + ((r[0] + r[1]) + (r[2] + r[3])));
@@ -315,34 +313,34 @@ __global__ void __launch_bounds__(kThreads, 1)
     // ---- policy conv1x1 256->73 over B -> logits [slot][ch*64 + cell]
     {
         const int q = lane >> 4, col = lane & 15;
-        f32x4 pa[kPolCT][kTPW];
+        f32x4 pa[kPolCT][TPW];
 #pragma unroll
         for (int c = 0; c < kPolCT; ++c) {
             const float4 b = *(const float4 *)(W.b_p2 + c * 16 + 4 * q);
 #pragma unroll
-            for (int u = 0; u < kTPW; ++u) pa[c][u] = f32x4{b.x, b.y, b.z, b.w};
+            for (int u = 0; u < TPW; ++u) pa[c][u] = f32x4{b.x, b.y, b.z, b.w};
         }
 #pragma unroll 2
         for (int ks = 0; ks < 8; ++ks) {
-            uint4 a[kPolCT], b[kTPW];
+            uint4 a[kPolCT], b[TPW];
 #pragma unroll
             for (int c = 0; c < kPolCT; ++c) a[c] = W.w_p2[((size_t)ks * kPolCT + c) * kFrag + lane];
 #pragma unroll
-            for (int u = 0; u < kTPW; ++u) {
-                const int t = kTPW * wave + u;
+            for (int u = 0; u < TPW; ++u) {
+                const int t = TPW * wave + u;
                 const int v = (t >> 2) * 64 + (t & 3) * 16 + col;
                 b[u] = *(const uint4 *)(smem + kBufB + row_chunk(v, 4 * ks + q));
             }
 #pragma unroll
             for (int c = 0; c < kPolCT; ++c)
 #pragma unroll
-                for (int u = 0; u < kTPW; ++u)
+                for (int u = 0; u < TPW; ++u)
                     pa[c][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[c]), as_bf16x8(b[u]), pa[c][u], 0,
                                                                        0, 0);
         }
 #pragma unroll
-        for (int u = 0; u < kTPW; ++u) {
-            const int t = kTPW * wave + u;
+        for (int u = 0; u < TPW; ++u) {
+            const int t = TPW * wave + u;
             const uint32_t slot = slot0 + (t >> 2);
             const int cell = (t & 3) * 16 + col;
             if (slot < count) {
@@ -356,6 +354,26 @@ __global__ void __launch_bounds__(kThreads, 1)
                     }
             }
         }
+    }
+}
+
+// P = 2 positions per workgroup, or 1 when there are no more positions than
+// CUs (the small batches of a game's tail: the same work per CU, half the
+// latency).  A position's results do not depend on P.
+__global__ void __launch_bounds__(kThreads, 1)
+    k_chess_forward(const uint32_t *__restrict__ d_count, uint32_t max_n, uint32_t n_cu,
+                    const uint16_t *__restrict__ x, NetW W, float *__restrict__ logits, float *__restrict__ value) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kSmem];
+    const uint32_t count = d_count ? min(*d_count, max_n) : max_n;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (count <= n_cu) {
+        if (blockIdx.x >= count) return;
+        forward_body<1>(smem, count, blockIdx.x, x, W, logits, value, tid, lane, wave);
+    } else {
+        const uint32_t slot0 = blockIdx.x * 2;
+        if (slot0 >= count) return;
+        forward_body<2>(smem, count, slot0, x, W, logits, value, tid, lane, wave);
     }
 }
 
@@ -580,7 +598,8 @@ static NetW weights_of(const spai_chess_net *n) {
 int net_eval(spai_chess_net *net, hipStream_t st, const uint32_t *d_count, uint32_t max_n, const uint16_t *x,
              float *logits, float *value) {
     if (!max_n) return SPAI_OK;
-    k_chess_forward<<<(max_n + kPos - 1) / kPos, kThreads, 0, st>>>(d_count, max_n, x, weights_of(net), logits, value);
+    k_chess_forward<<<max_n, kThreads, 0, st>>>(d_count, max_n, (uint32_t)net->eng->n_cu, x, weights_of(net), logits,
+                                                value);
     SPAI_HIP(hipGetLastError());
     return SPAI_OK;
 }

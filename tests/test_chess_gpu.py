@@ -166,6 +166,22 @@ def test_chess_net_vs_torch_golden(ch, sc):
     eng.close()
 
 
+def test_chess_net_positions_per_workgroup_invariance(ch, sc):
+    # > #CUs positions run 2 per workgroup, <= #CUs run 1 per workgroup: a
+    # position's logits and value must not depend on which
+    rng = np.random.default_rng(4)
+    x = (rng.random((300, 19, 8, 8)) < 0.2).astype(np.float32)
+    eng = sc.ChessEngine(num_searches=4, max_trees=8)
+    net = sc.ChessNet(eng, 2, sc.init_params(2, 1))
+    lg2, v2 = net.forward(x)
+    lg1, v1 = net.forward(x[:37])
+    assert np.array_equal(lg1, lg2[:37]) and np.array_equal(v1, v2[:37])
+    lg3, v3 = net.forward(x[250:300])
+    assert np.array_equal(lg3, lg2[250:300]) and np.array_equal(v3, v2[250:300])
+    net.close()
+    eng.close()
+
+
 def test_chess_net_20_blocks_vs_fp64(ch, sc):
     rng = random.Random(9)
     xs = []
