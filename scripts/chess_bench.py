@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--cpu-games", type=int, default=32)
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r01", "chess", "forward_traffic.json"),
+                    help="PMC summary (scripts/gpu_chess_traffic.sh): HBM bytes per k_chess_forward launch")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -185,6 +187,14 @@ def main():
     fpe = flops_per_eval(args.blocks)
     leaves = items[1] / max(1.0, launches[1])
     achieved = fpe * leaves / (ms[1] * 1e-3) / 1e12 if ms[1] > 0 else None
+    traffic, traffic_src = None, None
+    if os.path.exists(args.traffic_json):   # measured by separate rocprofv3 --pmc passes of this workload
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        if "k_chess_forward" in tj:
+            traffic = tj["k_chess_forward"]["hbm_bytes_per_launch"]
+            traffic_src = ("%s: (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch over %d launches (FETCH doubled for "
+                           "gfx950)" % (os.path.relpath(args.traffic_json, REPO), tj["k_chess_forward"]["launches"]))
     result = {
         "metric": "MCTS sims/sec, chess 400 sims/move (BASELINE.json config 4)",
         "value": sims / dt, "unit": "sims/s", "n_gpus": 1, "higher_is_better": True, "dtype": "bf16",
@@ -198,7 +208,8 @@ def main():
         "kernel_ms": {"select_leaf": ms[0], "forward": ms[1], "expand": ms[2]},
         "roofline": {"bound": "mfma", "kernel": "k_chess_forward (fused %dx256 ResNet)" % args.blocks,
                      "achieved": achieved, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / BF16_PEAK_TFLOPS if achieved else None, "traffic": None,
+                     "frac": achieved / BF16_PEAK_TFLOPS if achieved else None, "traffic": traffic,
+                     "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                      "flop_per_eval": fpe, "avg_leaves_per_launch": leaves, "avg_launch_ms": ms[1]},
     }
     net.close()
