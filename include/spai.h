@@ -129,6 +129,22 @@ int spai_predict(spai_net *net, uint32_t n, const spai_c4_state *states, float *
 /* Evaluator that search uses when cfg.eval == SPAI_EVAL_NET (Mcts.model, mcts.rs:41-44) */
 int spai_engine_set_net(spai_engine *eng, spai_net *net);
 
+/* ------------------------------------------------------------------ policy
+ * Policy trait methods (game/mod.rs:35-44) on a flat policy array (Connect4 7,
+ * TicTacToe 9, chess 4672 = get_flat_ndarray order).  Host functions.  For
+ * chess, map the index to a move with spai_chess_index_move (get_action). */
+/* Policy::normalize (connect_four.rs:96-98, chess.rs:518-520): p /= ndarray sum(p) */
+int spai_policy_normalize(float *p, uint32_t n);
+/* Policy::get_best_action (connect_four.rs:116-124, chess.rs:535-545): index of
+ * the LAST maximum under f32::total_cmp (NaN above +inf, -0 below +0) */
+int spai_policy_best_action(const float *p, uint32_t n, uint32_t *index);
+/* Policy::sample (connect_four.rs:104-114, chess.rs:526-533): WeightedIndex
+ * (rand 0.8) over p^temperature with f32 running totals.  u01 in [0, 1) is the
+ * uniform that rand's UniformFloat<f32> draws, ((u32 >> 9) as f32) * 2^-23, so a
+ * caller feeding its own rng's u32 reproduces rand's choice exactly.
+ * SPAI_ERR_INVALID for an empty policy, a negative/NaN weight or all-zero weights. */
+int spai_policy_sample(const float *p, uint32_t n, float temperature, float u01, uint32_t *index);
+
 /* ------------------------------------------------------------------ search
  * Tree (mcts.rs:32-39,67-89,161-192) + Mcts::search (mcts.rs:196-332).
  * Trees live in HBM; node ids are per-tree handles (stable across
@@ -365,6 +381,10 @@ int spai_chess_net_create(spai_chess *e, int blocks, const float *params, size_t
 int spai_chess_net_destroy(spai_chess_net *net);
 /* Net::forward(x, train=false): x [n][19][8][8] -> logits [n][4672], value [n] */
 int spai_chess_net_forward(spai_chess_net *net, uint32_t n, const float *x, float *logits, float *value);
+/* Model::predict (model/mod.rs:36-98) over game slots [first, first+n): encoding
+ * (with each slot's repetition count), forward, softmax, mask_invalid_actions ->
+ * priors [n][4672], values [n]; all on the device. */
+int spai_chess_predict(spai_chess_net *net, uint32_t first, uint32_t n, float *priors, float *values);
 int spai_chess_set_net(spai_chess *e, spai_chess_net *net);
 
 /* search: Tree (mcts.rs) + Mcts::search over chess trees held on the device.
@@ -422,6 +442,8 @@ int spai_ttt_net_init_params(int blocks, uint64_t seed, float *params);
 int spai_ttt_net_create(spai_ttt *e, int blocks, const float *params, size_t n_params, spai_ttt_net **out);
 int spai_ttt_net_destroy(spai_ttt_net *net);
 int spai_ttt_net_forward(spai_ttt_net *net, uint32_t n, const float *x, float *logits, float *value);
+/* Model::predict over game slots [first, first+n) -> priors [n][9], values [n] */
+int spai_ttt_predict(spai_ttt_net *net, uint32_t first, uint32_t n, float *priors, float *values);
 int spai_ttt_set_net(spai_ttt *e, spai_ttt_net *net);
 int spai_ttt_trees_create(spai_ttt *e, uint32_t n);
 /* per tree i: policy [i][9], child_ids / child_visits [i][9], n_children [i] (any may be NULL) */

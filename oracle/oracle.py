@@ -65,6 +65,8 @@ def lib():
         L.or_uniform.restype = d
         L.or_uniform.argtypes = [u64, u64, u64]
         L.or_weighted_index.argtypes = [fp, i, f, d]
+        L.or_policy_best_action.argtypes = [fp, i]
+        L.or_policy_sample.argtypes = [fp, i, f, f]
         L.or_splitmix64.restype = u64
         L.or_splitmix64.argtypes = [u64]
         L.or_hash_eval_raw.argtypes = [u64, u64, i, i, fp, fp]

@@ -354,6 +354,61 @@ int or_weighted_index(const float *visits, int n, float temperature, double u) {
     return n - 1;
 }
 
+/* Policy::get_best_action (connect_four.rs:116-124): Iterator::max_by with
+ * f32::total_cmp returns the last of equal maxima.  total_cmp (Rust core,
+ * f32.rs): left ^= ((left >> 31) as u32 >> 1) as i32 on the bit patterns, then
+ * signed comparison. */
+static int total_cmp_f32(float a, float b) {
+    int32_t l, r;
+    memcpy(&l, &a, 4);
+    memcpy(&r, &b, 4);
+    l ^= (int32_t)(((uint32_t)(l >> 31)) >> 1);
+    r ^= (int32_t)(((uint32_t)(r >> 31)) >> 1);
+    return (l > r) - (l < r);
+}
+
+int or_policy_best_action(const float *p, int n) {
+    int best = -1;
+    for (int i = 0; i < n; ++i)
+        if (best < 0 || total_cmp_f32(p[best], p[i]) <= 0) best = i;   /* max_by: ties -> later */
+    return best;
+}
+
+/* Policy::sample (connect_four.rs:104-114): rand 0.8.5 WeightedIndex<f32> over
+ * mapv(powf(temperature)).  new(): total = w0; for each later w, push total,
+ * total += w (f32).  UniformFloat<f32>::new(0, total) shrinks scale one ulp at a
+ * time while scale * (1 - 2^-23) >= total; sample = u01 * scale + 0; the index
+ * is the number of pushed totals <= that sample.  Returns -1 (NoItem /
+ * InvalidWeight / AllWeightsZero / overflow, all panics in the reference). */
+int or_policy_sample(const float *p, int n, float temperature, float u01) {
+    if (n <= 0) return -1;
+    float total = 0.0f;
+    for (int i = 0; i < n; ++i) {
+        float w = powf(p[i], temperature);
+        if (!(w >= 0.0f)) return -1;
+        total = i == 0 ? w : total + w;
+    }
+    if (total == 0.0f || isinf(total)) return -1;
+    float scale = total;
+    for (;;) {
+        float top = scale * (1.0f - 1.1920929e-7f);
+        if (!(top >= total)) break;
+        uint32_t b;
+        memcpy(&b, &scale, 4);
+        b -= 1;
+        memcpy(&scale, &b, 4);
+    }
+    float chosen = u01 * scale + 0.0f;
+    int idx = 0;
+    float run = 0.0f;
+    for (int i = 0; i + 1 < n; ++i) {
+        float w = powf(p[i], temperature);
+        run = i == 0 ? w : run + w;
+        if (run <= chosen) idx = i + 1;
+    }
+    return idx;
+}
+
 /* ========================================================================
  * Deterministic stub evaluators.  Not part of the reference: they replace the
  * net in search/self-play parity tests so visit counts are an exact function

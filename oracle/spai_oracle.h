@@ -100,6 +100,9 @@ int or_ttt_next_state(const or_ttt_state *s, int action, or_ttt_state *out);
 void or_philox4x32(uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 double or_uniform(uint64_t seed, uint64_t game_id, uint64_t move_no);
 int or_weighted_index(const float *visits, int n, float temperature, double u);
+/* Policy::get_best_action / Policy::sample on a flat policy (game/mod.rs:42-43) */
+int or_policy_best_action(const float *p, int n);
+int or_policy_sample(const float *p, int n, float temperature, float u01);
 
 /* ---- deterministic stub evaluators (shared definition with the device) ---- */
 enum { OR_EVAL_NET = 0, OR_EVAL_UNIFORM = 1, OR_EVAL_HASH = 2 };

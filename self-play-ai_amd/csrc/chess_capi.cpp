@@ -239,6 +239,16 @@ int spai_chess_net_forward(spai_chess_net *net, uint32_t n, const float *x, floa
     return net_forward_host(net, n, x, logits, value);
 }
 
+int spai_chess_predict(spai_chess_net *net, uint32_t first, uint32_t n, float *priors, float *values) {
+    CH_PTR(net);
+    CH_CHECK(net->eng);
+    if (n) {
+        CH_PTR(priors);
+        CH_PTR(values);
+    }
+    return net_predict(net, first, n, priors, values);
+}
+
 int spai_chess_set_net(spai_chess *e, spai_chess_net *net) {
     CH_CHECK(e);
     SPAI_CHECK(!net || net->eng == e, SPAI_ERR_INVALID, "net belongs to another engine");

@@ -109,6 +109,9 @@ int slots_status(spai_chess *e, uint32_t first, uint32_t n, uint8_t *status, uin
                  uint8_t *terminated);
 int slots_encode(spai_chess *e, uint32_t first, uint32_t n, float *out);
 int slots_mask(spai_chess *e, uint32_t first, uint32_t n, const float *policy, uint32_t len, float *out);
+// device-pointer forms used by net_predict (chess_net.hip)
+int slots_encode_device(spai_chess *e, uint32_t first, uint32_t n, float *d_out);   // f32 [n][19][64]
+int slots_softmax_mask_device(spai_chess *e, uint32_t first, uint32_t n, const float *d_logits, float *d_out);
 Board from_abi(const spai_chess_state &s);
 spai_chess_state to_abi(const Board &b, uint32_t reps);
 void encode_host(const Board &b, uint32_t reps, float *out);   // [19][8][8]
@@ -123,6 +126,7 @@ void net_destroy(spai_chess_net *net);
 int net_eval(spai_chess_net *net, hipStream_t st, const uint32_t *d_count, uint32_t max_n, const uint16_t *x,
              float *logits, float *value);
 int net_forward_host(spai_chess_net *net, uint32_t n, const float *x, float *logits, float *value);
+int net_predict(spai_chess_net *net, uint32_t first, uint32_t n, float *priors, float *values);
 
 // chess_search.hip
 int trees_create(spai_chess *e, uint32_t n);

@@ -624,5 +624,31 @@ int net_forward_host(spai_chess_net *net, uint32_t n, const float *x, float *log
     return SPAI_OK;
 }
 
+// Model::predict (model/mod.rs:36-98) over game slots [first, first+n): encode
+// (with the slot's repetition count), forward, softmax, mask_invalid_actions,
+// all on the device; only the priors and values cross to the host.
+int net_predict(spai_chess_net *net, uint32_t first, uint32_t n, float *priors, float *values) {
+    if (!n) return SPAI_OK;
+    spai_chess *e = net->eng;
+    SPAI_CHECK((uint64_t)first + n <= e->slots.n, SPAI_ERR_INVALID, "slots [%u, %u) out of range (%u)", first,
+               first + n, e->slots.n);
+    if (net->io_cap < n) {
+        SPAI_TRY(net->io_x.alloc((size_t)n * 64 * kInCh));
+        SPAI_TRY(net->io_logits.alloc((size_t)n * kPolicy));
+        SPAI_TRY(net->io_value.alloc(n));
+        net->io_cap = n;
+    }
+    float *d_enc = e->slots.f32.p, *d_pri = e->slots.f32b.p;
+    SPAI_TRY(slots_encode_device(e, first, n, d_enc));
+    k_pack_input<<<(n * 64 + 255) / 256, 256, 0, e->stream>>>(d_enc, n, net->io_x.p);
+    SPAI_HIP(hipGetLastError());
+    SPAI_TRY(net_eval(net, e->stream, nullptr, n, net->io_x.p, net->io_logits.p, net->io_value.p));
+    SPAI_TRY(slots_softmax_mask_device(e, first, n, net->io_logits.p, d_pri));
+    SPAI_HIP(hipMemcpyAsync(priors, d_pri, sizeof(float) * n * kPolicy, hipMemcpyDeviceToHost, e->stream));
+    SPAI_HIP(hipMemcpyAsync(values, net->io_value.p, sizeof(float) * n, hipMemcpyDeviceToHost, e->stream));
+    SPAI_HIP(hipStreamSynchronize(e->stream));
+    return SPAI_OK;
+}
+
 }  // namespace chess
 }  // namespace spai

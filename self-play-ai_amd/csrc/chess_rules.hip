@@ -119,21 +119,15 @@ __global__ void k_slots_encode(const Board *__restrict__ boards, const uint64_t 
 
 // mask_invalid_actions (chess.rs:252-275): p * mask, then / ndarray sum (the
 // 8-way unrolled fold of numeric_util, as oracle/spai_oracle.c or_nd_sum), so
-// the result is bit-identical to the reference's arithmetic.  One wave per slot.
-__global__ void __launch_bounds__(64) k_slots_mask(const Board *__restrict__ boards, uint32_t first, uint32_t n,
-                                                   const float *__restrict__ pol, float *out) {
-    __shared__ float m[kPolicy];
-    __shared__ float part[8];
-    const int lane = threadIdx.x;
-    const uint32_t i = blockIdx.x;
-    if (i >= n) return;
-    const Board b = boards[first + i];
-    const float *p = pol + (size_t)i * kPolicy;
-    for (int j = lane; j < kPolicy; j += 64) m[j] = p[j] * 0.0f;
+// the result is bit-identical to the reference's arithmetic given p.  One wave
+// per slot; prob(j) yields the unmasked policy entry j.
+template <class P>
+__device__ __forceinline__ void masked_normalize(const Board &b, int lane, P &&prob, float *m, float *part, float *o) {
+    for (int j = lane; j < kPolicy; j += 64) m[j] = prob(j) * 0.0f;
     __syncthreads();
     wave_movegen(b, lane, [&](int, int mv) {
         const int idx = policy_index(b.side, mv);
-        m[idx] = p[idx] * 1.0f;
+        m[idx] = prob(idx) * 1.0f;
     });
     __syncthreads();
     if (lane < 8) {
@@ -147,8 +141,41 @@ __global__ void __launch_bounds__(64) k_slots_mask(const Board *__restrict__ boa
     sum = sum + (part[1] + part[5]);
     sum = sum + (part[2] + part[6]);
     sum = sum + (part[3] + part[7]);
-    float *o = out + (size_t)i * kPolicy;
     for (int j = lane; j < kPolicy; j += 64) o[j] = m[j] / sum;
+}
+
+__global__ void __launch_bounds__(64) k_slots_mask(const Board *__restrict__ boards, uint32_t first, uint32_t n,
+                                                   const float *__restrict__ pol, float *out) {
+    __shared__ float m[kPolicy];
+    __shared__ float part[8];
+    const int lane = threadIdx.x;
+    const uint32_t i = blockIdx.x;
+    if (i >= n) return;
+    const float *p = pol + (size_t)i * kPolicy;
+    masked_normalize(boards[first + i], lane, [&](int j) { return p[j]; }, m, part, out + (size_t)i * kPolicy);
+}
+
+// Model::predict's tail (model/mod.rs:62-93): softmax(-1) over the 4672 logits
+// (same reduction order as k_cexpand, so predict and search see the same
+// priors), then mask_invalid_actions.
+__global__ void __launch_bounds__(64) k_slots_softmax_mask(const Board *__restrict__ boards, uint32_t first,
+                                                           uint32_t n, const float *__restrict__ logits, float *out) {
+    __shared__ float m[kPolicy];
+    __shared__ float part[8];
+    const int lane = threadIdx.x;
+    const uint32_t i = blockIdx.x;
+    if (i >= n) return;
+    const float *lg = logits + (size_t)i * kPolicy;
+    float mx = -INFINITY;
+    for (int j = lane; j < kPolicy; j += 64) mx = fmaxf(mx, lg[j]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    float se = 0.0f;
+    for (int j = lane; j < kPolicy; j += 64) se += expf(lg[j] - mx);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o, 64);
+    masked_normalize(boards[first + i], lane, [&](int j) { return expf(lg[j] - mx) / se; }, m, part,
+                     out + (size_t)i * kPolicy);
 }
 
 }  // namespace
@@ -377,6 +404,24 @@ int slots_mask(spai_chess *e, uint32_t first, uint32_t n, const float *policy, u
     SPAI_HIP(hipGetLastError());
     SPAI_HIP(hipMemcpyAsync(out, S.f32b.p, sizeof(float) * kPolicy * n, hipMemcpyDeviceToHost, e->stream));
     SPAI_HIP(hipStreamSynchronize(e->stream));
+    return SPAI_OK;
+}
+
+int slots_encode_device(spai_chess *e, uint32_t first, uint32_t n, float *d_out) {
+    RANGE_CHECK(e, first, n);
+    if (!n) return SPAI_OK;
+    Slots &S = e->slots;
+    k_slots_encode<<<(n + kWavesPerBlock - 1) / kWavesPerBlock, 64 * kWavesPerBlock, 0, e->stream>>>(
+        S.board.p, S.hist.p, S.n_hist.p, S.max_hist, first, n, d_out);
+    SPAI_HIP(hipGetLastError());
+    return SPAI_OK;
+}
+
+int slots_softmax_mask_device(spai_chess *e, uint32_t first, uint32_t n, const float *d_logits, float *d_out) {
+    RANGE_CHECK(e, first, n);
+    if (!n) return SPAI_OK;
+    k_slots_softmax_mask<<<n, 64, 0, e->stream>>>(e->slots.board.p, first, n, d_logits, d_out);
+    SPAI_HIP(hipGetLastError());
     return SPAI_OK;
 }
 

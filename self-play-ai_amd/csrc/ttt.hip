@@ -108,6 +108,15 @@ SPAI_HD void stub_raw(int kind, const State &s, float *raw, float *value) {
     *value = (float)((int)((h >> 48) & 255) - 127) / 128.0f;
 }
 
+// softmax(-1) of the 9 logits (model/mod.rs:63), as the search's expand step
+__device__ inline void softmax9(const float *l, float *raw) {
+    float mx = l[0];
+    for (int a = 1; a < kCells; ++a) mx = fmaxf(mx, l[a]);
+    float se = 0.0f;
+    for (int a = 0; a < kCells; ++a) se += expf(l[a] - mx);
+    for (int a = 0; a < kCells; ++a) raw[a] = expf(l[a] - mx) / se;
+}
+
 // mask_invalid_actions (tictactoe.rs:218-236): p * mask / ndarray sum
 SPAI_HD void mask9(uint32_t lg, const float *p, float *out) {
     float m[kCells];
@@ -314,12 +323,7 @@ __global__ __launch_bounds__(64) void k_texpand(TV T, BV B, uint32_t max_n, cons
     const int n = __builtin_popcount(lg);
     float pri[kCells], raw[kCells], v;
     if (kind == SPAI_EVAL_NET) {   // softmax(-1) then mask (model/mod.rs:62-93)
-        const float *l = B.logits + (size_t)s * kCells;
-        float mx = l[0];
-        for (int a = 1; a < kCells; ++a) mx = fmaxf(mx, l[a]);
-        float se = 0.0f;
-        for (int a = 0; a < kCells; ++a) se += expf(l[a] - mx);
-        for (int a = 0; a < kCells; ++a) raw[a] = expf(l[a] - mx) / se;
+        softmax9(B.logits + (size_t)s * kCells, raw);
         v = B.value[s];
     } else {
         stub_raw(kind, st, raw, &v);
@@ -382,7 +386,12 @@ __global__ void k_tslots(State *g, uint32_t first, uint32_t n, int op, const int
     if (op == 0) mask[i] = legal(s);
     else if (op == 1) rc[i] = apply(s, in[i]);
     else if (op == 2) encode(s, fout + (size_t)i * 27);
-    else mask9(legal(s), fin + (size_t)i * 9, fout + (size_t)i * 9);
+    else if (op == 3) mask9(legal(s), fin + (size_t)i * 9, fout + (size_t)i * 9);
+    else {   // Model::predict's tail: softmax, then mask_invalid_actions
+        float raw[kCells];
+        softmax9(fin + (size_t)i * 9, raw);
+        mask9(legal(s), raw, fout + (size_t)i * 9);
+    }
 }
 
 // ---------------------------------------------------------------- engine
@@ -802,6 +811,33 @@ int spai_ttt_net_forward(spai_ttt_net *net, uint32_t n, const float *x, float *l
     SPAI_HIP(hipGetLastError());
     SPAI_HIP(hipMemcpyAsync(logits, net->io_l.p, 36ull * n, hipMemcpyDeviceToHost, e->stream));
     SPAI_HIP(hipMemcpyAsync(value, net->io_v.p, 4ull * n, hipMemcpyDeviceToHost, e->stream));
+    SPAI_HIP(hipStreamSynchronize(e->stream));
+    return SPAI_OK;
+}
+
+// Model::predict (model/mod.rs:36-98) over game slots [first, first+n)
+int spai_ttt_predict(spai_ttt_net *net, uint32_t first, uint32_t n, float *priors, float *values) {
+    T_PTR(net);
+    T_CHECK(net->eng);
+    spai_ttt *e = static_cast<spai_ttt *>(net->eng);
+    SPAI_CHECK((uint64_t)first + n <= e->n_slots, SPAI_ERR_INVALID, "slots [%u, %u) out of range (%u)", first,
+               first + n, e->n_slots);
+    if (!n) return SPAI_OK;
+    T_PTR(priors);
+    T_PTR(values);
+    if (net->io_cap < n) {
+        SPAI_TRY(net->io_x.alloc((size_t)n * 27));
+        SPAI_TRY(net->io_l.alloc((size_t)n * 9));
+        SPAI_TRY(net->io_v.alloc(n));
+        net->io_cap = n;
+    }
+    const uint32_t g = (n + 63) / 64;
+    k_tslots<<<g, 64, 0, e->stream>>>(e->slots.p, first, n, 2, nullptr, nullptr, nullptr, net->io_x.p, nullptr);
+    k_tnet<<<n, 64, 0, e->stream>>>(nullptr, n, net->io_x.p, wview(net), net->io_l.p, net->io_v.p);
+    k_tslots<<<g, 64, 0, e->stream>>>(e->slots.p, first, n, 4, nullptr, nullptr, nullptr, e->sf2.p, net->io_l.p);
+    SPAI_HIP(hipGetLastError());
+    SPAI_HIP(hipMemcpyAsync(priors, e->sf2.p, 36ull * n, hipMemcpyDeviceToHost, e->stream));
+    SPAI_HIP(hipMemcpyAsync(values, net->io_v.p, 4ull * n, hipMemcpyDeviceToHost, e->stream));
     SPAI_HIP(hipStreamSynchronize(e->stream));
     return SPAI_OK;
 }

@@ -37,18 +37,20 @@ SYMBOLS = [
     "spai_learner_set_comm", "spai_params_save_safetensors", "spai_params_load_safetensors",
     "spai_replay_create", "spai_replay_destroy", "spai_replay_push", "spai_replay_pop", "spai_replay_size",
     "spai_choose_multiple", "spai_pipeline_config_default", "spai_pipeline_run", "spai_learner_train",
+    "spai_policy_normalize", "spai_policy_best_action", "spai_policy_sample",
     # chess (spai_chess.py)
     "spai_chess_config_default", "spai_chess_create", "spai_chess_destroy", "spai_chess_sync",
     "spai_chess_games_resize", "spai_chess_games_write", "spai_chess_games_read", "spai_chess_legal_moves",
     "spai_chess_apply", "spai_chess_status", "spai_chess_encode", "spai_chess_mask_invalid",
     "spai_chess_move_index", "spai_chess_index_move", "spai_chess_net_num_params", "spai_chess_net_init_params",
-    "spai_chess_net_create", "spai_chess_net_destroy", "spai_chess_net_forward", "spai_chess_set_net",
+    "spai_chess_net_create", "spai_chess_net_destroy", "spai_chess_net_forward", "spai_chess_predict", "spai_chess_set_net",
     "spai_chess_trees_create", "spai_chess_search", "spai_chess_tree_use_subtree", "spai_chess_tree_root", "spai_chess_trees_advance",
     "spai_chess_selfplay_run", "spai_chess_set_timing", "spai_chess_timing",
     # tictactoe (spai_ttt.py)
     "spai_ttt_create", "spai_ttt_destroy", "spai_ttt_games_resize", "spai_ttt_games_write", "spai_ttt_games_read",
     "spai_ttt_legal_mask", "spai_ttt_apply", "spai_ttt_encode", "spai_ttt_mask_invalid", "spai_ttt_net_num_params",
     "spai_ttt_net_init_params", "spai_ttt_net_create", "spai_ttt_net_destroy", "spai_ttt_net_forward",
+    "spai_ttt_predict",
     "spai_ttt_set_net", "spai_ttt_trees_create", "spai_ttt_search", "spai_ttt_tree_use_subtree",
     "spai_ttt_selfplay_run",
 ]
@@ -166,6 +168,9 @@ def lib():
         L.spai_choose_multiple.argtypes = [u32, u32, u64, u64, vp]
         L.spai_pipeline_config_default.argtypes = [P(PipelineConfig)]
         L.spai_pipeline_run.argtypes = [P(PipelineConfig), vp, C.c_size_t, P(PipelineStats)]
+        L.spai_policy_normalize.argtypes = [vp, u32]
+        L.spai_policy_best_action.argtypes = [vp, u32, P(u32)]
+        L.spai_policy_sample.argtypes = [vp, u32, C.c_float, C.c_float, P(u32)]
         _lib = L
     return _lib
 
@@ -505,6 +510,29 @@ def choose_multiple(n, k, seed=0, stream=0):
     out = np.zeros(min(n, k), np.uint32)
     _check(lib().spai_choose_multiple(n, k, seed, stream, _p(out)))
     return out
+
+
+def policy_normalize(p):
+    """Policy::normalize (game/mod.rs:40) of a flat f32 policy; returns a new array"""
+    a = np.array(p, np.float32, copy=True).ravel()
+    _check(lib().spai_policy_normalize(_p(a), a.size))
+    return a
+
+
+def policy_best_action(p):
+    """Policy::get_best_action: last index of the f32::total_cmp maximum"""
+    a = np.ascontiguousarray(p, np.float32).ravel()
+    out = C.c_uint32()
+    _check(lib().spai_policy_best_action(_p(a), a.size, C.byref(out)))
+    return out.value
+
+
+def policy_sample(p, temperature, u01):
+    """Policy::sample: WeightedIndex over p^temperature at the uniform draw u01 in [0, 1)"""
+    a = np.ascontiguousarray(p, np.float32).ravel()
+    out = C.c_uint32()
+    _check(lib().spai_policy_sample(_p(a), a.size, temperature, u01, C.byref(out)))
+    return out.value
 
 
 def pipeline_run(init_params, selfplay_devices=(0,), learner_device=0, checkpoint_dir=None, **kw):

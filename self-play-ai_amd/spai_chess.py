@@ -52,6 +52,7 @@ def lib():
         L.spai_chess_net_create.argtypes = [vp, i32, vp, C.c_size_t, P(vp)]
         L.spai_chess_net_destroy.argtypes = [vp]
         L.spai_chess_net_forward.argtypes = [vp, u32, vp, vp, vp]
+        L.spai_chess_predict.argtypes = [vp, u32, u32, vp, vp]
         L.spai_chess_set_net.argtypes = [vp, vp]
         L.spai_chess_trees_create.argtypes = [vp, u32]
         L.spai_chess_search.argtypes = [vp, u32, vp, u32, vp, vp, vp, vp, vp]
@@ -273,3 +274,10 @@ class ChessNet:
         v = np.zeros(n, np.float32)
         _check(lib().spai_chess_net_forward(self.h, n, _p(x), _p(lg), _p(v)))
         return lg, v
+
+    def predict(self, n, first=0):
+        """Model::predict over the engine's game slots [first, first+n)"""
+        pr = np.zeros((n, POLICY), np.float32)
+        v = np.zeros(n, np.float32)
+        _check(lib().spai_chess_predict(self.h, first, n, _p(pr), _p(v)))
+        return pr, v

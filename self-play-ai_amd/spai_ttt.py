@@ -33,6 +33,7 @@ def lib():
         L.spai_ttt_net_create.argtypes = [vp, i32, vp, C.c_size_t, P(vp)]
         L.spai_ttt_net_destroy.argtypes = [vp]
         L.spai_ttt_net_forward.argtypes = [vp, u32, vp, vp, vp]
+        L.spai_ttt_predict.argtypes = [vp, u32, u32, vp, vp]
         L.spai_ttt_set_net.argtypes = [vp, vp]
         L.spai_ttt_trees_create.argtypes = [vp, u32]
         L.spai_ttt_search.argtypes = [vp, u32, vp, u32, vp, vp, vp, vp]
@@ -177,3 +178,10 @@ class TTTNet:
         v = np.zeros(n, np.float32)
         _check(lib().spai_ttt_net_forward(self.h, n, _p(x), _p(lg), _p(v)))
         return lg, v
+
+    def predict(self, n, first=0):
+        """Model::predict over the engine's game slots [first, first+n)"""
+        pr = np.zeros((n, 9), np.float32)
+        v = np.zeros(n, np.float32)
+        _check(lib().spai_ttt_predict(self.h, first, n, _p(pr), _p(v)))
+        return pr, v

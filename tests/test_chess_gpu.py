@@ -149,6 +149,48 @@ def test_chess_mask_invalid_bit_exact(ch, sc):
     eng.close()
 
 
+def test_chess_predict_matches_forward_softmax_mask(ch, sc):
+    # Model::predict (model/mod.rs:36-98) on the device = encode -> forward ->
+    # softmax -> mask_invalid_actions; checked against the same device forward
+    # on the device encoding, softmax in fp64 and the oracle's mask: |dp| <= 1e-6,
+    # support == the legal moves exactly, values bit-identical to forward.
+    rng = random.Random(9)
+    states = []
+    for g in range(20):
+        s = ch.ChessState()
+        for _ in range(rng.randrange(0, 60)):
+            mv = s.valid_actions()
+            if not mv or s.status:
+                break
+            s = s.next_state(rng.choice(mv))
+        if not s.status:
+            states.append(s)
+    eng = sc.ChessEngine(num_searches=4, max_trees=4)
+    eng.games_resize(len(states) + 2)
+    eng.games_write(np.array([_abi_state(s.st) for s in states], sc.STATE_DTYPE), first=2)
+    net = sc.ChessNet(eng, 2, sc.init_params(2, 3))
+    pr, v = net.predict(len(states), first=2)
+    x = eng.encode(len(states), first=2)
+    lg, vf = net.forward(x)
+    assert np.array_equal(v, vf)
+    for i, s in enumerate(states):
+        z = lg[i].astype(np.float64)
+        sm = np.exp(z - z.max())
+        sm = (sm / sm.sum()).astype(np.float32)
+        ref = s.mask_invalid(sm)
+        assert np.abs(pr[i] - ref).max() <= 1e-6, i
+        legal = s.mask_invalid(np.ones(4672, np.float32)) > 0
+        assert np.array_equal(pr[i] > 0, legal), i
+        assert abs(float(pr[i].sum(dtype=np.float64)) - 1.0) <= 1e-5
+    pr0, _ = net.predict(1)   # slot 0: the start position
+    assert (pr0[0] > 0).sum() == 20
+    with pytest.raises(sc.SpaiError):
+        net.predict(len(states) + 3)
+    ch.arena_reset()
+    net.close()
+    eng.close()
+
+
 def test_chess_net_vs_torch_golden(ch, sc):
     g = np.load(os.path.join(GOLDEN, "chess_net_b1.npz"))
     blocks = int(g["blocks"])

@@ -86,6 +86,34 @@ def test_ttt_net_vs_torch_golden(st):
     eng.close()
 
 
+def test_ttt_predict_matches_forward_softmax_mask(oracle, st):
+    # Model::predict over slots: encode -> forward -> softmax -> mask (fp32 device)
+    rng = random.Random(4)
+    n = 64
+    eng = st.TTTEngine()
+    eng.games_resize(n)
+    for ply in range(rng.randrange(0, 4) + 2):
+        mask = eng.legal_mask(n)
+        acts = [rng.choice([a for a in range(9) if (m >> a) & 1]) if m else 0 for m in mask]
+        eng.apply(acts, check=False)
+    st_arr = eng.games_read(n)
+    live = [i for i in range(n) if st_arr[i]["status"] == 0]
+    net = st.TTTNet(eng, 2, st.init_params(2, 5))
+    pr, v = net.predict(n)
+    lg, vf = net.forward(eng.encode(n))
+    assert np.array_equal(v, vf)
+    mask = eng.legal_mask(n)
+    for i in live:
+        z = lg[i].astype(np.float64)
+        sm = np.exp(z - z.max())
+        sm /= sm.sum()
+        m = sm * np.array([(mask[i] >> a) & 1 for a in range(9)])
+        assert np.abs(pr[i] - m / m.sum()).max() <= 1e-6, i
+        assert np.array_equal(pr[i] > 0, m > 0)
+    net.close()
+    eng.close()
+
+
 def _oracle_search(oracle, n, sims):
     L = oracle.lib()
     trees = [L.or_tree_create(oracle.GAME_TICTACTOE) for _ in range(n)]
