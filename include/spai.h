@@ -363,6 +363,10 @@ int spai_chess_status(spai_chess *e, uint32_t first, uint32_t n, uint8_t *status
                       uint8_t *terminated);
 /* get_encoding: out [n][19][8][8] f32 */
 int spai_chess_encode(spai_chess *e, uint32_t first, uint32_t n, float *out);
+/* Device time (HIP events, mean of iters launches) of the batched rules kernels
+ * over slots [first, first+n): ms[0] legal move lists + counts + status,
+ * ms[1] encoding.  Measurement only; slots are not modified. */
+int spai_chess_rules_bench(spai_chess *e, uint32_t first, uint32_t n, uint32_t iters, double *ms);
 /* mask_invalid_actions (chess.rs:252-275): policy [n][len] -> out [n][4672]; len must be 4672 */
 int spai_chess_mask_invalid(spai_chess *e, uint32_t first, uint32_t n, const float *policy, uint32_t len,
                             float *out);

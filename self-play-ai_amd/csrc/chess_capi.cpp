@@ -167,6 +167,12 @@ int spai_chess_status(spai_chess *e, uint32_t first, uint32_t n, uint8_t *status
     return slots_status(e, first, n, status, reps, value, terminated);
 }
 
+int spai_chess_rules_bench(spai_chess *e, uint32_t first, uint32_t n, uint32_t iters, double *ms) {
+    CH_CHECK(e);
+    CH_PTR(ms);
+    return slots_rules_bench(e, first, n, iters, ms);
+}
+
 int spai_chess_encode(spai_chess *e, uint32_t first, uint32_t n, float *out) {
     CH_CHECK(e);
     if (n) CH_PTR(out);

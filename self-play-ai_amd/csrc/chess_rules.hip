@@ -407,6 +407,45 @@ int slots_mask(spai_chess *e, uint32_t first, uint32_t n, const float *policy, u
     return SPAI_OK;
 }
 
+// Device time of the batched rules kernels over the current slots [first, first+n):
+// ms[0] legal move lists + counts + status (k_slots_status), ms[1] f32 encoding
+// (k_slots_encode); mean of `iters` launches after one warm-up launch.
+int slots_rules_bench(spai_chess *e, uint32_t first, uint32_t n, uint32_t iters, double *ms) {
+    RANGE_CHECK(e, first, n);
+    SPAI_CHECK(n > 0 && iters > 0, SPAI_ERR_INVALID, "rules_bench needs n, iters > 0");
+    Slots &S = e->slots;
+    hipEvent_t ev[2];
+    SPAI_HIP(hipEventCreate(&ev[0]));
+    SPAI_HIP(hipEventCreate(&ev[1]));
+    const uint32_t grid = (n + kWavesPerBlock - 1) / kWavesPerBlock;
+    int rc = SPAI_OK;
+    for (int k = 0; k < 2 && rc == SPAI_OK; ++k) {
+        double tot = 0;
+        for (uint32_t it = 0; it <= iters; ++it) {
+            if (hipEventRecord(ev[0], e->stream) != hipSuccess) rc = SPAI_ERR_DEVICE;
+            if (k == 0)
+                k_slots_status<<<grid, 64 * kWavesPerBlock, 0, e->stream>>>(S.board.p, S.hist.p, S.n_hist.p,
+                                                                            S.max_hist, first, n, S.moves.p,
+                                                                            S.u32.p, (uint8_t *)S.i32.p, nullptr);
+            else
+                k_slots_encode<<<grid, 64 * kWavesPerBlock, 0, e->stream>>>(S.board.p, S.hist.p, S.n_hist.p,
+                                                                            S.max_hist, first, n, S.f32.p);
+            float t = 0;
+            if (hipGetLastError() != hipSuccess || hipEventRecord(ev[1], e->stream) != hipSuccess ||
+                hipEventSynchronize(ev[1]) != hipSuccess || hipEventElapsedTime(&t, ev[0], ev[1]) != hipSuccess) {
+                set_error("chess rules bench launch failed");
+                rc = SPAI_ERR_DEVICE;
+                break;
+            }
+            if (it) tot += t;
+        }
+        ms[k] = tot / iters;
+    }
+    (void)hipEventDestroy(ev[0]);
+    (void)hipEventDestroy(ev[1]);
+    return rc;
+}
+
 int slots_encode_device(spai_chess *e, uint32_t first, uint32_t n, float *d_out) {
     RANGE_CHECK(e, first, n);
     if (!n) return SPAI_OK;

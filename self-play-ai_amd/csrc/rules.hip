@@ -51,6 +51,83 @@ __global__ void k_apply(uint64_t *__restrict__ x, uint64_t *__restrict__ o, uint
     rc[i] = (int8_t)(e == 0 ? SPAI_OK : e == -2 ? SPAI_ERR_ILLEGAL_MOVE : e == -3 ? SPAI_ERR_GAME_OVER : SPAI_ERR_INVALID);
 }
 
+// Four games per lane (slot range starting at a multiple of 4): 32-B x/o loads,
+// 4-B status/count/result words, so each lane keeps 4x the bytes in flight of the
+// one-game kernels above (which handle unaligned ranges).
+__global__ void k_legal4(const uint64_t *__restrict__ x, const uint64_t *__restrict__ o,
+                         const uint8_t *__restrict__ st, uint8_t *__restrict__ mask, uint32_t first, uint32_t cnt) {
+    const uint32_t i = 4u * (blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= cnt) return;
+    const uint32_t g = first + i;
+    if (i + 4 <= cnt) {
+        const ulonglong2 xa = *(const ulonglong2 *)(x + g), xb = *(const ulonglong2 *)(x + g + 2);
+        const ulonglong2 oa = *(const ulonglong2 *)(o + g), ob = *(const ulonglong2 *)(o + g + 2);
+        const uint32_t s4 = *(const uint32_t *)(st + g);
+        *(uint32_t *)(mask + i) = c4::legal_mask(xa.x, oa.x, (uint8_t)s4) |
+                                  c4::legal_mask(xa.y, oa.y, (uint8_t)(s4 >> 8)) << 8 |
+                                  c4::legal_mask(xb.x, ob.x, (uint8_t)(s4 >> 16)) << 16 |
+                                  c4::legal_mask(xb.y, ob.y, (uint8_t)(s4 >> 24)) << 24;
+    } else {
+        for (uint32_t k = i; k < cnt; ++k) mask[k] = (uint8_t)c4::legal_mask(x[first + k], o[first + k], st[first + k]);
+    }
+}
+
+__device__ __forceinline__ int8_t apply_rc(int e) {
+    return (int8_t)(e == 0 ? SPAI_OK : e == -2 ? SPAI_ERR_ILLEGAL_MOVE : e == -3 ? SPAI_ERR_GAME_OVER : SPAI_ERR_INVALID);
+}
+
+__global__ void k_apply4(uint64_t *__restrict__ x, uint64_t *__restrict__ o, uint8_t *__restrict__ n,
+                         uint8_t *__restrict__ st, const int32_t *__restrict__ act, int8_t *__restrict__ rc,
+                         uint32_t first, uint32_t cnt) {
+    const uint32_t i = 4u * (blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= cnt) return;
+    const uint32_t g = first + i;
+    if (i + 4 <= cnt) {
+        uint64_t xs[4], os[4];
+        *(ulonglong2 *)xs = *(const ulonglong2 *)(x + g);
+        *(ulonglong2 *)(xs + 2) = *(const ulonglong2 *)(x + g + 2);
+        *(ulonglong2 *)os = *(const ulonglong2 *)(o + g);
+        *(ulonglong2 *)(os + 2) = *(const ulonglong2 *)(o + g + 2);
+        uint32_t n4 = *(const uint32_t *)(n + g), s4 = *(const uint32_t *)(st + g);
+        const int4 a4 = *(const int4 *)(act + i);
+        const int a[4] = {a4.x, a4.y, a4.z, a4.w};
+        uint32_t r4 = 0, nn = 0, ss = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            c4::State s{xs[k], os[k], (uint8_t)(n4 >> (8 * k)), (uint8_t)(s4 >> (8 * k))}, r;
+            const int e = c4::next_state(s, a[k], r);
+            if (e == 0) {
+                xs[k] = r.x;
+                os[k] = r.o;
+                s = r;
+            }
+            nn |= (uint32_t)s.n << (8 * k);
+            ss |= (uint32_t)s.status << (8 * k);
+            r4 |= (uint32_t)(uint8_t)apply_rc(e) << (8 * k);
+        }
+        *(ulonglong2 *)(x + g) = *(const ulonglong2 *)xs;
+        *(ulonglong2 *)(x + g + 2) = *(const ulonglong2 *)(xs + 2);
+        *(ulonglong2 *)(o + g) = *(const ulonglong2 *)os;
+        *(ulonglong2 *)(o + g + 2) = *(const ulonglong2 *)(os + 2);
+        *(uint32_t *)(n + g) = nn;
+        *(uint32_t *)(st + g) = ss;
+        *(uint32_t *)(rc + i) = r4;
+    } else {
+        for (uint32_t k = i; k < cnt; ++k) {
+            const uint32_t gk = first + k;
+            c4::State s{x[gk], o[gk], n[gk], st[gk]}, r;
+            const int e = c4::next_state(s, act[k], r);
+            if (e == 0) {
+                x[gk] = r.x;
+                o[gk] = r.o;
+                n[gk] = r.n;
+                st[gk] = r.status;
+            }
+            rc[k] = apply_rc(e);
+        }
+    }
+}
+
 __global__ void k_value_term(const uint8_t *__restrict__ st, float *__restrict__ v, uint8_t *__restrict__ t,
                              uint32_t first, uint32_t cnt) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -60,37 +137,48 @@ __global__ void k_value_term(const uint8_t *__restrict__ st, float *__restrict__
     t[i] = s != c4::kOngoing;
 }
 
-// plane value of element e (0..125) of a game's [3][6][7] encoding
-__device__ __forceinline__ uint32_t enc_bit(uint64_t mine, uint64_t theirs, int e) {
-    int plane = e / c4::kCells, cell = e - plane * c4::kCells;
-    int row = cell / c4::kCols, col = cell - row * c4::kCols;
-    int b = col * 7 + row;
-    uint64_t occ = mine | theirs;
-    uint64_t src = plane == 0 ? mine : plane == 1 ? theirs : ~occ;
-    return (uint32_t)((src >> b) & 1ull);
-}
-
-// f32 encoding, one lane per float2 (63 per game)
-__global__ void k_encode_f32(const uint64_t *__restrict__ x, const uint64_t *__restrict__ o,
-                             const uint8_t *__restrict__ n, float2 *__restrict__ out, uint32_t first, uint32_t cnt) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (uint64_t)cnt * 63) return;
-    uint32_t gi = (uint32_t)(i / 63), w = (uint32_t)(i % 63);
-    uint32_t g = first + gi;
-    bool xm = c4::x_to_move(n[g]);
-    uint64_t mine = xm ? x[g] : o[g], theirs = xm ? o[g] : x[g];
-    out[i] = make_float2((float)enc_bit(mine, theirs, 2 * w), (float)enc_bit(mine, theirs, 2 * w + 1));
-}
-
-// bf16 encoding (the layout the NN stem would read), one lane per 2 x bf16
-__global__ void k_encode_bf16(const uint64_t *__restrict__ x, const uint64_t *__restrict__ o,
-                              const uint8_t *__restrict__ n, uint32_t *__restrict__ out, uint32_t cnt) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (uint64_t)cnt * 63) return;
-    uint32_t g = (uint32_t)(i / 63), w = (uint32_t)(i % 63);
-    bool xm = c4::x_to_move(n[g]);
-    uint64_t mine = xm ? x[g] : o[g], theirs = xm ? o[g] : x[g];
-    out[i] = (enc_bit(mine, theirs, 2 * w) ? 0x3F80u : 0u) | (enc_bit(mine, theirs, 2 * w + 1) ? 0x3F800000u : 0u);
+// get_encoding (connect_four.rs:242-259): [3][6][7] planes (mine, theirs,
+// empty) of the player to move; element e = plane*42 + row*7 + col reads bit
+// col*7 + row.  One wave per 64 games: each lane builds its game's output words
+// in LDS (stride D words, odd, so the writes are conflict-free), then the wave
+// stores the 64 games' contiguous D*256-byte run with 16-B coalesced stores.
+// BF16: D = 63 words of 2 bf16 (the layout the net stem would read); else D = 126 f32.
+template <bool BF16>
+__global__ __launch_bounds__(64) void k_encode(const uint64_t *__restrict__ x, const uint64_t *__restrict__ o,
+                                               const uint8_t *__restrict__ n, uint32_t *__restrict__ out,
+                                               uint32_t first, uint32_t cnt) {
+    constexpr int D = BF16 ? 63 : 126;
+    __shared__ uint32_t buf[64 * D];
+    const int lane = threadIdx.x;
+    const uint32_t g0 = blockIdx.x * 64u;
+    const uint32_t ng = min(64u, cnt - g0);
+    if ((uint32_t)lane < ng) {
+        const uint32_t g = first + g0 + lane;
+        const bool xm = c4::x_to_move(n[g]);
+        const uint64_t xv = x[g], ov = o[g];
+        const uint64_t mine = xm ? xv : ov, theirs = xm ? ov : xv;
+        const uint64_t pl[3] = {mine, theirs, ~(mine | theirs)};
+        uint32_t *dst = buf + lane * D;
+#pragma unroll
+        for (int w = 0; w < D; ++w) {
+            if (BF16) {
+                const int e0 = 2 * w, e1 = 2 * w + 1;
+                const int c0 = e0 % 42, c1 = e1 % 42;
+                const uint32_t b0 = (uint32_t)(pl[e0 / 42] >> ((c0 % 7) * 7 + c0 / 7)) & 1u;
+                const uint32_t b1 = (uint32_t)(pl[e1 / 42] >> ((c1 % 7) * 7 + c1 / 7)) & 1u;
+                dst[w] = (b0 ? 0x3F80u : 0u) | (b1 ? 0x3F800000u : 0u);
+            } else {
+                const int c = w % 42;
+                dst[w] = ((pl[w / 42] >> ((c % 7) * 7 + c / 7)) & 1u) ? 0x3F800000u : 0u;
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t words = ng * D;
+    uint32_t *base = out + (size_t)g0 * D;
+    const uint32_t v4 = words / 4;   // g0 * D * 4 B is a multiple of 16 B (64 | g0)
+    for (uint32_t j = lane; j < v4; j += 64) *(uint4 *)(base + 4 * j) = *(const uint4 *)(buf + 4 * j);
+    for (uint32_t j = 4 * v4 + lane; j < words; j += 64) base[j] = buf[j];
 }
 
 __global__ void k_mask(const uint64_t *__restrict__ x, const uint64_t *__restrict__ o,
@@ -205,7 +293,10 @@ int rules_legal(spai_engine *e, uint32_t first, uint32_t n, uint32_t *mask) {
     DevBuf<uint8_t> d;
     SPAI_TRY(d.alloc(n));
     GameSlots &g = e->games;
-    k_legal<<<blocks_for(n), kBlock, 0, e->stream>>>(g.x.p, g.o.p, g.status.p, d.p, first, n);
+    if (first % 4 == 0)
+        k_legal4<<<blocks_for((n + 3) / 4), kBlock, 0, e->stream>>>(g.x.p, g.o.p, g.status.p, d.p, first, n);
+    else
+        k_legal<<<blocks_for(n), kBlock, 0, e->stream>>>(g.x.p, g.o.p, g.status.p, d.p, first, n);
     SPAI_HIP(hipGetLastError());
     std::vector<uint8_t> h(n);
     SPAI_HIP(hipMemcpyAsync(h.data(), d.p, n, hipMemcpyDeviceToHost, e->stream));
@@ -224,7 +315,11 @@ int rules_apply(spai_engine *e, uint32_t first, uint32_t n, const int32_t *actio
     SPAI_TRY(dr.alloc(n));
     SPAI_HIP(hipMemcpyAsync(da.p, actions, n * 4, hipMemcpyHostToDevice, e->stream));
     GameSlots &g = e->games;
-    k_apply<<<blocks_for(n), kBlock, 0, e->stream>>>(g.x.p, g.o.p, g.n.p, g.status.p, da.p, dr.p, first, n);
+    if (first % 4 == 0)
+        k_apply4<<<blocks_for((n + 3) / 4), kBlock, 0, e->stream>>>(g.x.p, g.o.p, g.n.p, g.status.p, da.p, dr.p,
+                                                                    first, n);
+    else
+        k_apply<<<blocks_for(n), kBlock, 0, e->stream>>>(g.x.p, g.o.p, g.n.p, g.status.p, da.p, dr.p, first, n);
     SPAI_HIP(hipGetLastError());
     std::vector<int8_t> h(n);
     SPAI_HIP(hipMemcpyAsync(h.data(), dr.p, n, hipMemcpyDeviceToHost, e->stream));
@@ -262,7 +357,7 @@ int rules_encode(spai_engine *e, uint32_t first, uint32_t n, float *out) {
     DevBuf<float> d;
     SPAI_TRY(d.alloc((size_t)n * 126));
     GameSlots &g = e->games;
-    k_encode_f32<<<blocks_for((uint64_t)n * 63), kBlock, 0, e->stream>>>(g.x.p, g.o.p, g.n.p, (float2 *)d.p, first, n);
+    k_encode<false><<<(n + 63) / 64, 64, 0, e->stream>>>(g.x.p, g.o.p, g.n.p, (uint32_t *)d.p, first, n);
     SPAI_HIP(hipGetLastError());
     SPAI_HIP(hipMemcpyAsync(out, d.p, (size_t)n * 126 * 4, hipMemcpyDeviceToHost, e->stream));
     SPAI_HIP(hipStreamSynchronize(e->stream));
@@ -300,9 +395,19 @@ int rules_bench(spai_engine *e, uint32_t n, uint32_t iters, double *ms) {
     SPAI_TRY(act.alloc(n));
     SPAI_TRY(rc.alloc(n));
     SPAI_TRY(enc.alloc((size_t)n * 63));
+    DevBuf<uint64_t> x0, o0;   // pristine positions: every timed apply starts from them
+    DevBuf<uint8_t> nn0, st0;
+    SPAI_TRY(x0.alloc(n));
+    SPAI_TRY(o0.alloc(n));
+    SPAI_TRY(nn0.alloc(n));
+    SPAI_TRY(st0.alloc(n));
     hipStream_t s = e->stream;
     k_random_positions<<<blocks_for(n), kBlock, 0, s>>>(x.p, o.p, nn.p, st.p, n, 12345);
     SPAI_HIP(hipGetLastError());
+    SPAI_HIP(hipMemcpyAsync(x0.p, x.p, 8ull * n, hipMemcpyDeviceToDevice, s));
+    SPAI_HIP(hipMemcpyAsync(o0.p, o.p, 8ull * n, hipMemcpyDeviceToDevice, s));
+    SPAI_HIP(hipMemcpyAsync(nn0.p, nn.p, n, hipMemcpyDeviceToDevice, s));
+    SPAI_HIP(hipMemcpyAsync(st0.p, st.p, n, hipMemcpyDeviceToDevice, s));
     {
         std::vector<int32_t> a(n);
         for (uint32_t i = 0; i < n; ++i) a[i] = (int32_t)((i * 2654435761u) % 7);
@@ -314,14 +419,19 @@ int rules_bench(spai_engine *e, uint32_t n, uint32_t iters, double *ms) {
     for (int k = 0; k < 3; ++k) {
         float best = 0;
         for (uint32_t it = 0; it < iters + 1; ++it) {   // first launch is warmup
+            if (k == 1) {   // restore the positions (outside the timed region) so every apply does its writes
+                SPAI_HIP(hipMemcpyAsync(x.p, x0.p, 8ull * n, hipMemcpyDeviceToDevice, s));
+                SPAI_HIP(hipMemcpyAsync(o.p, o0.p, 8ull * n, hipMemcpyDeviceToDevice, s));
+                SPAI_HIP(hipMemcpyAsync(nn.p, nn0.p, n, hipMemcpyDeviceToDevice, s));
+                SPAI_HIP(hipMemcpyAsync(st.p, st0.p, n, hipMemcpyDeviceToDevice, s));
+            }
             SPAI_HIP(hipEventRecord(ev[0], s));
             if (k == 0) {
-                k_legal<<<blocks_for(n), kBlock, 0, s>>>(x.p, o.p, st.p, mask.p, 0, n);
+                k_legal4<<<blocks_for((n + 3) / 4), kBlock, 0, s>>>(x.p, o.p, st.p, mask.p, 0, n);
             } else if (k == 1) {
-                // apply to a copy-free stream: re-applying on already advanced slots is fine for timing
-                k_apply<<<blocks_for(n), kBlock, 0, s>>>(x.p, o.p, nn.p, st.p, act.p, rc.p, 0, n);
+                k_apply4<<<blocks_for((n + 3) / 4), kBlock, 0, s>>>(x.p, o.p, nn.p, st.p, act.p, rc.p, 0, n);
             } else {
-                k_encode_bf16<<<blocks_for((uint64_t)n * 63), kBlock, 0, s>>>(x.p, o.p, nn.p, enc.p, n);
+                k_encode<true><<<(n + 63) / 64, 64, 0, s>>>(x.p, o.p, nn.p, enc.p, 0, n);
             }
             SPAI_HIP(hipGetLastError());
             SPAI_HIP(hipEventRecord(ev[1], s));

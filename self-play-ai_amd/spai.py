@@ -41,7 +41,7 @@ SYMBOLS = [
     # chess (spai_chess.py)
     "spai_chess_config_default", "spai_chess_create", "spai_chess_destroy", "spai_chess_sync",
     "spai_chess_games_resize", "spai_chess_games_write", "spai_chess_games_read", "spai_chess_legal_moves",
-    "spai_chess_apply", "spai_chess_status", "spai_chess_encode", "spai_chess_mask_invalid",
+    "spai_chess_apply", "spai_chess_status", "spai_chess_encode", "spai_chess_rules_bench", "spai_chess_mask_invalid",
     "spai_chess_move_index", "spai_chess_index_move", "spai_chess_net_num_params", "spai_chess_net_init_params",
     "spai_chess_net_create", "spai_chess_net_destroy", "spai_chess_net_forward", "spai_chess_predict", "spai_chess_set_net",
     "spai_chess_trees_create", "spai_chess_search", "spai_chess_tree_use_subtree", "spai_chess_tree_root", "spai_chess_trees_advance",

@@ -53,6 +53,7 @@ def lib():
         L.spai_chess_net_destroy.argtypes = [vp]
         L.spai_chess_net_forward.argtypes = [vp, u32, vp, vp, vp]
         L.spai_chess_predict.argtypes = [vp, u32, u32, vp, vp]
+        L.spai_chess_rules_bench.argtypes = [vp, u32, u32, u32, vp]
         L.spai_chess_set_net.argtypes = [vp, vp]
         L.spai_chess_trees_create.argtypes = [vp, u32]
         L.spai_chess_search.argtypes = [vp, u32, vp, u32, vp, vp, vp, vp, vp]
@@ -173,6 +174,12 @@ class ChessEngine:
         term = np.zeros(n, np.uint8)
         _check(lib().spai_chess_status(self.h, first, n, _p(st), _p(reps), _p(v), _p(term)))
         return st, reps, v, term
+
+    def rules_bench(self, n, first=0, iters=10):
+        """device ms per launch: [legal moves + status, encoding] over slots [first, first+n)"""
+        ms = np.zeros(2, np.float64)
+        _check(lib().spai_chess_rules_bench(self.h, first, n, iters, _p(ms)))
+        return ms
 
     def encode(self, n, first=0):
         out = np.zeros((n, 19, 8, 8), np.float32)

@@ -77,6 +77,70 @@ def test_rules_lockstep_random_games(spai, oracle):
     e.close()
 
 
+def test_rules_subranges_and_encoding_vs_oracle(spai, oracle):
+    """Slot sub-ranges at every alignment (the 4-games-per-lane kernels take
+    ranges starting at a multiple of 4, the scalar ones the rest; tails of 1-3
+    games) and the LDS-staged encoder against the oracle's get_encoding."""
+    n = 203
+    e = spai.Engine(num_searches=1, max_trees=1)
+    e.games_resize(n)
+    rng = np.random.default_rng(3)
+    for p in range(rng.integers(5, 30)):
+        lm = e.legal_mask(n)
+        r = rng.random((n, 7)) * ((lm[:, None] >> np.arange(7)) & 1)
+        e.apply(np.argmax(r, axis=1).astype(np.int32), check=False)
+    snap = e.games_read(n)
+    states = [_oracle_state(oracle, int(g["x"]), int(g["o"]), int(g["n"]), int(g["status"])) for g in snap]
+    enc = e.encode(n)
+    lm = e.legal_mask(n)
+    for i, s in enumerate(states):
+        assert np.array_equal(enc[i], s.encoding()), i
+        assert lm[i] == s.legal_mask(), i
+    acts = rng.integers(-1, 8, n).astype(np.int32)
+    for first in (0, 1, 2, 3, 4, 5, 8):
+        for cnt in (1, 3, 4, 7, 64, 65, 130):
+            if first + cnt > n:
+                continue
+            e.games_write(snap)
+            assert np.array_equal(e.legal_mask(cnt, first), lm[first:first + cnt])
+            assert np.array_equal(e.encode(cnt, first), enc[first:first + cnt])
+            rc = e.apply(acts[first:first + cnt], first=first, check=False)
+            after = e.games_read(n)
+            for k in range(n):
+                if first <= k < first + cnt:
+                    a = int(acts[k])
+                    s = states[k]
+                    if s.status != 0:
+                        assert rc[k - first] == -3
+                        exp = snap[k]
+                    elif not 0 <= a < 7:
+                        assert rc[k - first] == -1
+                        exp = snap[k]
+                    elif not (s.legal_mask() >> a) & 1:
+                        assert rc[k - first] == -2
+                        exp = snap[k]
+                    else:
+                        assert rc[k - first] == 0
+                        t = s.next_state(a)
+                        exp = _c4_record(spai, t)
+                    assert after[k].tobytes() == exp.tobytes(), (first, cnt, k)
+                else:
+                    assert after[k].tobytes() == snap[k].tobytes(), (first, cnt, k)
+    e.close()
+
+
+def _c4_record(spai, s):
+    x = o = 0
+    for col in range(7):
+        for row in range(6):
+            b = 1 << (col * 7 + row)
+            if s.st.board[row][col] == 1:
+                x |= b
+            elif s.st.board[row][col] == 2:
+                o |= b
+    return spai.states_array([(x, o, s.n, s.status)])[0]
+
+
 def test_rules_encode_mask_and_errors(spai, oracle):
     with open(os.path.join(GOLDEN, "rules_c4.json")) as f:
         traces = json.load(f)["traces"]
