@@ -57,9 +57,16 @@ constexpr int kZ = 0;                      // 256 B of zeros just below X (out-o
 constexpr int kX = 256;                    // [336][128 B] bf16 activations (256-B aligned)
 constexpr int kZ1 = kX + kP * 128;         // 256 B of zeros just below Y
 constexpr int kY = kZ1 + 256;              // second activation buffer
-constexpr int kLinK = 1472;                // 35 x 42 = 1470 head features, padded to 46 k-steps of 32
-constexpr int kLinKSteps = kLinK / 32;     // 46
-constexpr int kH = kY;                     // bf16 head features [8][1472] overlay Y
+// Head features in LDS: H[s][cell*36 + c] (c < 35: 32 policy + 3 value channels,
+// c = 35 is a zero pad), so the head conv's epilogue stores 4 channels of a cell
+// as one 8-B word.  The fused linear runs over this cell-major K order (the host
+// permutes the linear weights from the reference's c*42 + cell flatten to it).
+constexpr int kHC = 36;                    // channels per cell in H
+constexpr int kLinFeat = kHC * 42;         // 1512
+constexpr int kLinK = 1536;                // padded to 48 k-steps of 32
+constexpr int kLinKSteps = kLinK / 32;     // 48
+constexpr int kLinPitch = kLinK + 8;       // 3088-B rows: 16 rows hit 16 distinct 16-B bank groups
+constexpr int kH = kY;                     // bf16 head features [8][kLinPitch] overlay Y
 constexpr int kHBytes = kP * 128;          // (all of Y)
 constexpr int kB = kH + kHBytes;           // 8 x (mine, theirs)
 constexpr int kL = kB + kS * 16;           // linear partials [4 waves][8][8] f32
@@ -70,7 +77,7 @@ constexpr int kPlanes = kBias + kBiasFloats * 4;   // stem neighbour planes [8][
 constexpr int kWStem = kPlanes + kS * 32 * 8;      // stem weight fragments [4 ct][64 lanes] x 16 B, staged once
 constexpr int kLdsBytes = kWStem + 4 * 64 * 16;
 constexpr int kStamps = 20;                // phase stamps per wave in the diagnostic mode (17..19: inside block 0 conv1)
-static_assert(kS * kLinK * 2 <= kHBytes, "head features fit in Y");
+static_assert(kS * kLinPitch * 2 <= kHBytes, "head features fit in Y");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 
 struct NetParams {
@@ -90,6 +97,11 @@ struct NetParams {
 // Phase stamps exist only in the diagnostic build (-DSPAI_DIAG): the branch
 // around the store would otherwise cost the production kernel precise
 // vmcnt tracking (hipcc waits vmcnt(0) after such control flow).
+#ifdef SPAI_DIAG_HEAD
+constexpr bool kDiagHead = true;   // stamps 17..19 time the head instead of block 0 conv 1
+#else
+constexpr bool kDiagHead = false;
+#endif
 __device__ __forceinline__ void stamp(const NetParams &P, int wave, int lane, int k) {
 #ifdef SPAI_DIAG
     if (P.stamps && lane == 0) P.stamps[((size_t)blockIdx.x * kWaves + wave) * kStamps + k] = __builtin_amdgcn_s_memtime();
@@ -386,8 +398,20 @@ __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const fl
     epilogue_act<W, NPT, kX, false>(smem, g, acc);
 }
 
+constexpr int kLinPerWave = 12;
+template <int W>
+__device__ __forceinline__ void load_lin(const NetParams &P, int lane, uint4 (&wl)[kLinPerWave]) {
+    constexpr int k0 = kLinPerWave * W;
+#pragma unroll
+    for (int i = 0; i < kLinPerWave; ++i)
+        if (k0 + i < kLinKSteps) wl[i] = P.w_lin[(k0 + i) * 64 + lane];
+}
+
+#ifndef SPAI_LIN_LATE
+#define SPAI_LIN_LATE 0
+#endif
 template <int W, int S>
-__device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, int lane) {
+__device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, int lane, uint4 (&wl)[kLinPerWave]) {
     constexpr int NPT = npt_of(S);
     using PL = Plan<W, kHeadCT, NPT>;
     Geo<PL::NT> g;
@@ -398,21 +422,33 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
     load_a_first<kHeadCT, PL::C0, PL::CTL, DA>(P.w_head, lane, A);
     conv_mfma<W, kHeadCT, NPT, kX, DA, DB>(smem, g, (const float *)(smem + kBias) + kHid * (1 + 2 * P.blocks), P.w_head, P.w_head,
                               lane, A, acc);
+#ifdef SPAI_DIAG
+    if (kDiagHead) {
+        asm volatile("" ::"v"(acc[0][0]), "v"(acc[PL::n - 1][3]));
+        stamp(P, W, lane, 17);
+    }
+#endif
+    if (SPAI_LIN_LATE) load_lin<W>(P, lane, wl);
     const int col = lane & 15, q = lane >> 4;
     uint16_t *H = (uint16_t *)(smem + kH);
 #pragma unroll
     for (int i = 0; i < PL::n; ++i) {
-        const int co0 = PL::co(i) * 16 + 4 * q;
+        const int co0 = PL::co(i) * 16 + 4 * q;   // pad channels (zero weights and bias) come out as 0
         const int p = PL::gpt(PL::pt(i)) * 16 + col;
         const int s = p / c4::kCells, cell = p - s * c4::kCells;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int co = co0 + r;
-            if (co < kHeadC && (NPT * 16 == S * c4::kCells || s < S))
-                H[s * kLinK + co * c4::kCells + cell] = __builtin_bit_cast(uint16_t, (__bf16)fmaxf(acc[i][r], 0.f));
-        }
+        if (co0 < kHC && (NPT * 16 == S * c4::kCells || s < S))
+            *(uint2 *)(H + s * kLinPitch + cell * kHC + co0) =
+                make_uint2(pack_relu_bf16x2(acc[i][0], acc[i][1]), pack_relu_bf16x2(acc[i][2], acc[i][3]));
     }
-    if (W == 0 && lane < S * 2) H[(lane >> 1) * kLinK + kHeadC * c4::kCells + (lane & 1)] = 0;   // K padding
+    // K padding [1512, 1536) of each row: 6 words of 8 B
+    if (W == 0 && lane < S * 6)
+        *(uint2 *)(H + (lane / 6) * kLinPitch + kLinFeat + 4 * (lane % 6)) = make_uint2(0u, 0u);
+#ifdef SPAI_DIAG
+    if (kDiagHead) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        stamp(P, W, lane, 18);
+    }
+#endif
 }
 
 // fused policy|value linear on MFMA: out[s][o] = sum_k H[s][k] * Wl[o][k]
@@ -420,21 +456,12 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
 // 1344 <= k < 1470; connect_four.rs:63-64,69-70).  Wave W takes k-steps
 // [12W, 12W+12) of 46 (weights prefetched by load_lin before the head conv);
 // partial sums go to LDS.
-constexpr int kLinPerWave = 12;
-template <int W>
-__device__ __forceinline__ void load_lin(const NetParams &P, int lane, uint4 (&wl)[kLinPerWave]) {
-    constexpr int k0 = kLinPerWave * W;
-#pragma unroll
-    for (int i = 0; i < kLinPerWave; ++i)
-        if (k0 + i < kLinKSteps) wl[i] = P.w_lin[(k0 + i) * 64 + lane];
-}
-
 template <int W, int S>
 __device__ __forceinline__ void linear_mfma(uint8_t *smem, const uint4 (&wl)[kLinPerWave], int lane) {
     constexpr int k0 = kLinPerWave * W;
     constexpr int k1 = (kLinPerWave * (W + 1) < kLinKSteps) ? kLinPerWave * (W + 1) : kLinKSteps;
     const int s = lane & 15, q = lane >> 4;
-    const uint8_t *hrow = s < S ? smem + kH + s * kLinK * 2 + q * 16 : smem + kZ + q * 16;
+    const uint8_t *hrow = s < S ? smem + kH + s * kLinPitch * 2 + q * 16 : smem + kZ + q * 16;
     const int hstep = s < S ? 64 : 0;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -470,21 +497,21 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
         const int l1 = 2 * b, l2 = 2 * b + 1;
         conv_mfma<W, 4, NPT, kX, DA, DB>(smem, g, bias + kHid * (1 + l1), P.w_res + l1 * kLayer, P.w_res + l2 * kLayer, lane, A, acc);
 #ifdef SPAI_DIAG
-        if (b == 0) {   // make the k-loop's results visible before the stamp
+        if (b == 0 && !kDiagHead) {   // make the k-loop's results visible before the stamp
             asm volatile("" ::"v"(acc[0][0]), "v"(acc[PL4::n - 1][3]));
             stamp(P, W, lane, 17);
         }
 #endif
         epilogue_act<W, NPT, kY, false>(smem, g, acc);
 #ifdef SPAI_DIAG
-        if (b == 0) {
+        if (b == 0 && !kDiagHead) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             stamp(P, W, lane, 18);
         }
 #endif
         __syncthreads();
 #ifdef SPAI_DIAG
-        if (b == 0) stamp(P, W, lane, 19);
+        if (b == 0 && !kDiagHead) stamp(P, W, lane, 19);
 #endif
         if (l1 < 12) stamp(P, W, lane, 2 + l1);
         conv_mfma<W, 4, NPT, kY, DA, DB>(smem, g, bias + kHid * (1 + l2), P.w_res + l2 * kLayer,
@@ -494,8 +521,9 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
         if (l2 < 12) stamp(P, W, lane, 2 + l2);
     }
     uint4 wl[kLinPerWave];
-    load_lin<W>(P, lane, wl);
-    head_layer<W, S>(smem, P, lane);
+    if (kDiagHead) stamp(P, W, lane, 19);   // diagnostic head mode: 19 = before the head, 17 = head k-loop, 18 = H written
+    if (!SPAI_LIN_LATE) load_lin<W>(P, lane, wl);
+    head_layer<W, S>(smem, P, lane, wl);
     __syncthreads();
     stamp(P, W, lane, 14);
     linear_mfma<W, S>(smem, wl, lane);
@@ -779,16 +807,18 @@ int net_create(spai_engine *e, int blocks, int hidden, const float *params, size
     }
     up(n->w_head, wh);
     up(n->b_head, bh);
-    // fused linear as MFMA B fragments: [ks 46][lane 64][8], lane -> o = lane & 15,
-    // k = ks*32 + 8*(lane>>4) + j over the head features H[s][c*42 + cell]
+    // fused linear as MFMA B fragments: [ks 48][lane 64][8], lane -> o = lane & 15,
+    // k = ks*32 + 8*(lane>>4) + j over the head features H[s][cell*36 + c]; the
+    // reference flattens c*42 + cell (policy c < 32 -> logits 0..6, value c = 32..34 -> o = 7)
     std::vector<uint16_t> wlin((size_t)kLinKSteps * 64 * 8, 0);
     for (int ks = 0; ks < kLinKSteps; ++ks)
         for (int l = 0; l < 64; ++l)
             for (int j = 0; j < 8; ++j) {
                 const int o = l & 15, k = ks * 32 + 8 * (l >> 4) + j;
+                const int cell = k / kHC, c = k % kHC;
                 float v = 0.f;
-                if (o < 7 && k < kPolIn) v = pol_w[(size_t)o * kPolIn + k];
-                else if (o == 7 && k >= kPolIn && k < kPolIn + kValIn) v = val_w[k - kPolIn];
+                if (k < kLinFeat && o < 7 && c < 32) v = pol_w[(size_t)o * kPolIn + c * c4::kCells + cell];
+                else if (k < kLinFeat && o == 7 && c >= 32 && c < kHeadC) v = val_w[(c - 32) * c4::kCells + cell];
                 wlin[((size_t)ks * 64 + l) * 8 + j] = f2bf(v);
             }
     up(n->w_lin, wlin);
