@@ -285,7 +285,7 @@ int upload_roots(spai_engine *e, uint32_t t0, uint32_t n) {
     return SPAI_OK;
 }
 
-int timer_record(spai_engine *e, int which, uint32_t iter, bool begin) {
+int timer_record(spai_engine *e, int which, uint32_t iter, bool begin, hipStream_t st, int chain) {
     KernelTimer &K = e->timer;
     if (!K.enabled) return SPAI_OK;
     if (begin) {
@@ -298,29 +298,33 @@ int timer_record(spai_engine *e, int which, uint32_t iter, bool begin) {
         }
         K.which.push_back(which);
         K.iter.push_back(iter);
-        SPAI_HIP(hipEventRecord(K.ev[K.used], e->stream));
+        K.chain.push_back(chain);
+        SPAI_HIP(hipEventRecord(K.ev[K.used], st));
     } else {
-        SPAI_HIP(hipEventRecord(K.ev[K.used + 1], e->stream));
+        SPAI_HIP(hipEventRecord(K.ev[K.used + 1], st));
         K.used += 2;
     }
     return SPAI_OK;
 }
 
 // fold the sampled event pairs of one search call into the totals
-int timer_collect(spai_engine *e, const std::vector<uint32_t> &iter_counts, uint32_t n_active) {
+// ch_counts [chain][num_searches] leaves per iteration; n_active[chain] trees
+int timer_collect(spai_engine *e, const std::vector<uint32_t> &ch_counts, uint32_t num_searches,
+                  const uint32_t *n_active) {
     KernelTimer &K = e->timer;
     if (!K.enabled) return SPAI_OK;
     for (size_t i = 0; i < K.which.size(); ++i) {
         float ms = 0;
         SPAI_HIP(hipEventElapsedTime(&ms, K.ev[2 * i], K.ev[2 * i + 1]));
-        const int w = K.which[i];
+        const int w = K.which[i], h = K.chain[i];
         K.total_ms[w] += ms;
         K.launches[w] += 1;
-        K.items[w] += w == 0 ? n_active : iter_counts[K.iter[i]];
+        K.items[w] += w == 0 ? n_active[h] : ch_counts[(size_t)h * num_searches + K.iter[i]];
     }
     K.used = 0;
     K.which.clear();
     K.iter.clear();
+    K.chain.clear();
     return SPAI_OK;
 }
 
@@ -416,7 +420,7 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
         for (int h = 1; h < nchain; ++h) SPAI_HIP(hipStreamWaitEvent(e->chain_stream[h], e->ev_fork, 0));
     }
     const TreeView tv = tree_view(e);
-    const bool timed = e->timer.enabled;   // samples chain 0's launches
+    const bool timed = e->timer.enabled;   // samples every chain's launches every stride-th iteration
     for (uint32_t it = 0; it < num_searches; ++it) {
         const uint32_t cur = it & 1u;
         for (int h = 0; h < nchain; ++h) {
@@ -425,20 +429,20 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
             const BatchView bv = batch_view(e, h, cur);
             const uint32_t nh = cnt[h], g8 = (nh + kTreesPerBlock - 1) / kTreesPerBlock;
             const uint32_t *act = e->active.p + off[h];
-            const bool sample = timed && h == 0 && (it % e->timer.stride == 0);
-            if (sample) SPAI_TRY(timer_record(e, 0, it, true));
+            const bool sample = timed && (it % e->timer.stride == 0);
+            if (sample) SPAI_TRY(timer_record(e, 0, it, true, sh, h));
             k_select<<<g8, kBlock, 0, sh>>>(tv, bv, act, nh, e->cfg.c, e->err.p);
-            if (sample) SPAI_TRY(timer_record(e, 0, it, false));
-            if (sample) SPAI_TRY(timer_record(e, 1, it, true));
+            if (sample) SPAI_TRY(timer_record(e, 0, it, false, sh, h));
+            if (sample) SPAI_TRY(timer_record(e, 1, it, true, sh, h));
             if (kind == SPAI_EVAL_NET) {
                 SPAI_TRY(net_eval_batch(e->net, sh, bv.count, nh, B.mine.p, B.theirs.p, B.priors.p, B.value.p));
             } else {
                 k_eval_stub<<<(nh + kBlock - 1) / kBlock, kBlock, 0, sh>>>(bv, nh, kind);
             }
-            if (sample) SPAI_TRY(timer_record(e, 1, it, false));
-            if (sample) SPAI_TRY(timer_record(e, 2, it, true));
+            if (sample) SPAI_TRY(timer_record(e, 1, it, false, sh, h));
+            if (sample) SPAI_TRY(timer_record(e, 2, it, true, sh, h));
             k_expand<<<g8, kBlock, 0, sh>>>(tv, bv, nh, e->err.p, B.iter_counts.p + it, B.count.p + (cur ^ 1u));
-            if (sample) SPAI_TRY(timer_record(e, 2, it, false));
+            if (sample) SPAI_TRY(timer_record(e, 2, it, false, sh, h));
         }
     }
     SPAI_HIP(hipGetLastError());
@@ -457,7 +461,7 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
                                     num_searches * 4, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipMemcpyAsync(&err, e->err.p, 4, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipStreamSynchronize(st));
-    SPAI_TRY(timer_collect(e, ch_counts, cnt[0]));   // chain 0's launches and items
+    SPAI_TRY(timer_collect(e, ch_counts, num_searches, cnt));
     for (int h = 0; h < nchain; ++h)
         for (uint32_t i = 0; i < num_searches; ++i) counts[i] += ch_counts[(size_t)h * num_searches + i];
     SPAI_CHECK(!(err & kErrCapacity), SPAI_ERR_CAPACITY, "node arena full (cap %u per tree)", T.cap);

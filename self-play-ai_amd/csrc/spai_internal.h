@@ -109,6 +109,7 @@ struct KernelTimer {
     size_t used = 0;
     std::vector<int> which;         // kernel index per sampled launch
     std::vector<uint32_t> iter;     // iteration per sampled launch
+    std::vector<int> chain;         // search chain (stream) per sampled launch
 };
 
 }  // namespace spai
