@@ -239,7 +239,7 @@ def main():
         step(-1 - i)
     eng.sync()
     dist.barrier()
-    # HIP events on every 32nd search iteration of chain 0: ~0.6 % overhead (every
+    # HIP events on every 32nd search iteration of each chain: ~0.6 % overhead (every
     # 4th measured ~5 %: 31.9M vs 33.4M sims/s), ~1000 sampled launches per step
     eng.set_timing(not args.no_timing, stride=32)
     tot = dict(sims=0.0, games=0.0, evals=0.0, positions=0.0, moves=0.0)
@@ -294,6 +294,10 @@ def main():
                      "frac": achieved / BF16_PEAK_TFLOPS if achieved else None, "traffic": traffic,
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                      "flop_per_launch": per_launch_flop, "flop_per_eval": fpe,
+                     # whole-GPU view: every forward FLOP of the timed region over its wall time
+                     # (the two search chains' forwards overlap, so this is not per launch)
+                     "chip_achieved": evals / dt_max * fpe / 1e12 / dist.world,
+                     "chip_frac": evals / dt_max * fpe / 1e12 / dist.world / BF16_PEAK_TFLOPS,
                      "avg_launch_ms": ev["avg_ms"], "avg_leaves_per_launch": ev["items"] / max(1, ev["launches"])},
     }
     if args.rules_bench and dist.rank == 0:
