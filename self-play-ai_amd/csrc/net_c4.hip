@@ -333,6 +333,41 @@ __device__ __forceinline__ void epilogue_act(uint8_t *smem, const Geo<Plan<W, 4,
     }
 }
 
+// Residual add as one more MFMA per task: acc += I * x, B = the center-tap
+// fragment of the 32-channel block that holds the task's co tile (read from the
+// conv's output buffer, which still holds x), A = an identity selecting those 16
+// channels.  One exact product 1 * x plus zero products and a single fp32
+// rounding: the same value as the VALU add it replaces, for 8 issue cycles per
+// task instead of ~8 VALU instructions.  Another wave may be storing the other
+// 16 channels of the block meanwhile (co-major split); those lanes of B meet
+// zeros in A and the values are finite bf16 either way.
+#ifndef SPAI_RES_MFMA
+#define SPAI_RES_MFMA 1
+#endif
+template <int W, int NPT, int OUT>
+__device__ __forceinline__ void residual_mfma(const uint8_t *smem, const Geo<Plan<W, 4, NPT>::NT> &g, int lane,
+                                              f32x4 (&acc)[Plan<W, 4, NPT>::n]) {
+    using PL = Plan<W, 4, NPT>;
+    const int m = lane & 15, q = lane >> 4;
+    uint4 id[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int j = 16 * h + m - 8 * q;   // this lane's k slot that holds the 1, if any
+        uint32_t w[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = j == 2 * e ? 0x3F80u : j == 2 * e + 1 ? 0x3F800000u : 0u;
+        id[h] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    uint4 b[PL::n];
+#pragma unroll
+    for (int i = 0; i < PL::n; ++i)
+        b[i] = *(const uint4 *)(smem + OUT + (g.rel[PL::pt(i)][4] ^ ((PL::co(i) >> 1) << 6)));
+#pragma unroll
+    for (int i = 0; i < PL::n; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(id[PL::co(i) & 1]), as_bf16x8(b[i]), acc[i], 0, 0,
+                                                        0);
+}
+
 // stem: one k-step, k = tap*3 + plane (27 of 32 used).  Bitboard path: the
 // neighbour planes N[s][k] (one u64 per sample/tap/plane, built at kernel start)
 // hold at bit col*7+row the value of that cell's (dh,dw) neighbour, so lane
@@ -516,7 +551,12 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
         if (l1 < 12) stamp(P, W, lane, 2 + l1);
         conv_mfma<W, 4, NPT, kY, DA, DB>(smem, g, bias + kHid * (1 + l2), P.w_res + l2 * kLayer,
                             b + 1 < P.blocks ? P.w_res + (l2 + 1) * kLayer : P.w_res + l2 * kLayer, lane, A, acc);
-        epilogue_act<W, NPT, kX, true>(smem, g, acc);
+        if (SPAI_RES_MFMA) {
+            residual_mfma<W, NPT, kX>(smem, g, lane, acc);
+            epilogue_act<W, NPT, kX, false>(smem, g, acc);
+        } else {
+            epilogue_act<W, NPT, kX, true>(smem, g, acc);
+        }
         __syncthreads();
         if (l2 < 12) stamp(P, W, lane, 2 + l2);
     }
