@@ -231,6 +231,44 @@ __device__ __forceinline__ void epilogue(uint8_t *smem, int out, int wave, int l
         }
 }
 
+// Residual add as one identity MFMA per (co tile, cell tile): acc += I * x with
+// B = the (untapped) fragment of the 32-channel block holding the co tile, read
+// from the conv's output buffer (which still holds x), and A selecting the co
+// tile's 16 channels.  One exact product plus zeros and a single fp32 rounding:
+// the value of the VALU add it replaces.  Wave w owns co tiles 4w..4w+3, i.e.
+// whole 32-channel blocks, so no other wave writes them meanwhile.
+#ifndef SPAI_CHESS_RES_MFMA
+#define SPAI_CHESS_RES_MFMA 1
+#endif
+template <int NT>
+__device__ __forceinline__ void residual_mfma(const uint8_t *smem, int out, int wave, int lane,
+                                              f32x4 (&acc)[kCPW][NT]) {
+    const int m = lane & 15, q = lane >> 4, col = lane & 15;
+    uint4 id[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int j = 16 * h + m - 8 * q;   // this lane's k slot that holds the 1, if any
+        uint32_t w[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) w[e] = j == 2 * e ? 0x3F80u : j == 2 * e + 1 ? 0x3F800000u : 0u;
+        id[h] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+#pragma unroll
+    for (int c = 0; c < kCPW; ++c) {
+        const int ct = kCPW * wave + c;
+        uint4 b[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int v = (t >> 2) * 64 + (t & 3) * 16 + col;
+            b[t] = *(const uint4 *)(smem + out + row_chunk(v, (ct >> 1) * 4 + q));
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(id[ct & 1]), as_bf16x8(b[t]), acc[c][t], 0,
+                                                               0, 0);
+    }
+}
+
 // the forward of P positions (slots slot0 .. slot0+P-1) by one workgroup
 template <int P>
 __device__ __forceinline__ void forward_body(uint8_t *smem, uint32_t count, uint32_t slot0,
@@ -257,7 +295,12 @@ __device__ __forceinline__ void forward_body(uint8_t *smem, uint32_t count, uint
         epilogue<false, NT>(smem, kBufB, wave, lane, acc);
         __syncthreads();
         conv<9, 8, NT>(smem, kBufB, W.w_res + l2 * 72 * kCT * kFrag, W.b_res + l2 * kHid, wave, lane, acc);
-        epilogue<true, NT>(smem, kBufA, wave, lane, acc);
+        if (SPAI_CHESS_RES_MFMA) {
+            residual_mfma<NT>(smem, kBufA, wave, lane, acc);
+            epilogue<false, NT>(smem, kBufA, wave, lane, acc);
+        } else {
+            epilogue<true, NT>(smem, kBufA, wave, lane, acc);
+        }
         __syncthreads();
     }
     // ---- policy head: conv1x1 256->256 + ReLU -> buffer B
