@@ -971,7 +971,13 @@ int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
 int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint32_t max_n, const uint64_t *mine,
                    const uint64_t *theirs, float *priors, float *value) {
     if (!max_n) return SPAI_OK;
-    const uint32_t grid = std::min<uint32_t>(max_n, (uint32_t)net->n_cu);
+    // SPAI_FWD_GRID caps the persistent grid (tuning knob: fewer workgroups -> larger groups S)
+    static const uint32_t grid_cap = [] {
+        const char *v = std::getenv("SPAI_FWD_GRID");
+        return v ? (uint32_t)std::max(1, std::atoi(v)) : 0u;
+    }();
+    uint32_t grid = std::min<uint32_t>(max_n, (uint32_t)net->n_cu);
+    if (grid_cap) grid = std::min(grid, grid_cap);
     k_forward<false><<<grid, kThreads, 0, st>>>(d_count, max_n, 0, mine, theirs, nullptr, params_of(net), priors,
                                                 value, nullptr);
     SPAI_HIP(hipGetLastError());
