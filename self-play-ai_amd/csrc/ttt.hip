@@ -143,34 +143,52 @@ struct NetW {
     int blocks;
 };
 
-// 3x3 conv (pad 1) on a 3x3 board: thread t < co computes channel t at all 9 cells
+// 3x3 conv (pad 1) on a 3x3 board, 512 threads: wave g (of 8) accumulates input
+// channels [g*CI/8, (g+1)*CI/8) for output channel o = lane at all 9 cells (a
+// weight load feeds 9 FMAs; the wave's 64 loads are one coalesced 256-B read),
+// then thread t < co*9 sums the 8 partials in wave order.  Eight short
+// dependent load chains instead of one 64-deep chain per thread.
+constexpr int kNetWaves = 8;
+constexpr int kNetThreads = 64 * kNetWaves;   // 512
 template <int CI>
 __device__ __forceinline__ void conv3(const float *in, float *out, const float *wt, const float *b, int co, int t,
-                                      bool relu, const float *res) {
-    if (t >= co) return;
-    float acc[kCells];
-    for (int c = 0; c < kCells; ++c) acc[c] = b[t];
-    for (int ci = 0; ci < CI; ++ci)
-        for (int tap = 0; tap < 9; ++tap) {
-            const float w = wt[(ci * 9 + tap) * co + t];
-            const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+                                      bool relu, const float *res, float *part) {
+    const int o = t & 63, g = t >> 6;
+    constexpr int CPG = (CI + kNetWaves - 1) / kNetWaves;   // input channels per wave
+    if (o < co) {
+        float acc[kCells];
 #pragma unroll
-            for (int c = 0; c < kCells; ++c) {
-                const int y = c / 3 + dy, x = c % 3 + dx;
-                if ((unsigned)y < 3u && (unsigned)x < 3u) acc[c] = fmaf(w, in[ci * 9 + y * 3 + x], acc[c]);
+        for (int c = 0; c < kCells; ++c) acc[c] = 0.0f;
+        for (int ci = g * CPG; ci < CI && ci < (g + 1) * CPG; ++ci)
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const float w = wt[(ci * 9 + tap) * co + o];
+                const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+#pragma unroll
+                for (int c = 0; c < kCells; ++c) {
+                    const int y = c / 3 + dy, x = c % 3 + dx;
+                    if ((unsigned)y < 3u && (unsigned)x < 3u) acc[c] = fmaf(w, in[ci * 9 + y * 3 + x], acc[c]);
+                }
             }
-        }
-    for (int c = 0; c < kCells; ++c) {
-        float v = acc[c];
-        if (res) v += res[t * 9 + c];
-        out[t * 9 + c] = relu ? fmaxf(v, 0.0f) : v;
+#pragma unroll
+        for (int c = 0; c < kCells; ++c) part[(g * kHid + o) * kCells + c] = acc[c];
     }
+    __syncthreads();
+    for (int i = t; i < co * kCells; i += kNetThreads) {
+        float v = b[i / kCells];
+#pragma unroll
+        for (int gg = 0; gg < kNetWaves; ++gg) v += part[gg * kHid * kCells + i];
+        if (res) v += res[i];
+        out[i] = relu ? fmaxf(v, 0.0f) : v;
+    }
+    __syncthreads();
 }
 
-__global__ __launch_bounds__(64) void k_tnet(const uint32_t *__restrict__ d_count, uint32_t max_n,
-                                            const float *__restrict__ x, NetW W, float *__restrict__ logits,
-                                            float *__restrict__ value) {
+__global__ __launch_bounds__(kNetThreads) void k_tnet(const uint32_t *__restrict__ d_count, uint32_t max_n,
+                                                      const float *__restrict__ x, NetW W, float *__restrict__ logits,
+                                                      float *__restrict__ value) {
     __shared__ float a[kHid * 9], bb[kHid * 9], cc[kHid * 9], head[32 * 9 + 3 * 9];
+    __shared__ float part[kNetWaves * kHid * kCells];
     const uint32_t s = blockIdx.x;
     const uint32_t count = d_count ? min(*d_count, max_n) : max_n;
     if (s >= count) return;
@@ -178,31 +196,25 @@ __global__ __launch_bounds__(64) void k_tnet(const uint32_t *__restrict__ d_coun
     if (t < 27) cc[t] = x[(size_t)s * 27 + t];
     __syncthreads();
     const float *wt = W.wt, *b = W.b;
-    conv3<3>(cc, a, wt, b, kHid, t, true, nullptr);
+    conv3<3>(cc, a, wt, b, kHid, t, true, nullptr, part);
     wt += 27 * kHid;
     b += kHid;
-    __syncthreads();
     for (int l = 0; l < W.blocks; ++l) {
-        conv3<kHid>(a, bb, wt, b, kHid, t, true, nullptr);
+        conv3<kHid>(a, bb, wt, b, kHid, t, true, nullptr, part);
         wt += 576 * kHid;
         b += kHid;
-        __syncthreads();
-        conv3<kHid>(bb, cc, wt, b, kHid, t, true, a);   // relu(x + BN(conv(...)))
-        wt += 576 * kHid;
+        conv3<kHid>(bb, a, wt, b, kHid, t, true, a, part);   // relu(x + BN(conv(...))), in place: a is read before
+        wt += 576 * kHid;                                    // the partial-sum barrier, written after it
         b += kHid;
-        __syncthreads();
-        for (int i = t; i < kHid * 9; i += 64) a[i] = cc[i];
-        __syncthreads();
     }
-    conv3<kHid>(a, head, wt, b, 32, t, true, nullptr);                    // policy conv + BN + ReLU
-    conv3<kHid>(a, head + 288, wt + 576 * 32, b + 32, 3, t, true, nullptr);   // value conv + BN + ReLU
-    __syncthreads();
+    conv3<kHid>(a, head, wt, b, 32, t, true, nullptr, part);                        // policy conv + BN + ReLU
+    conv3<kHid>(a, head + 288, wt + 576 * 32, b + 32, 3, t, true, nullptr, part);   // value conv + BN + ReLU
     if (t < kCells) {   // flatten (c*9 + cell) + linear 288 -> 9
         float acc = W.pl_b[t];
         for (int k = 0; k < 288; ++k) acc = fmaf(W.pl_w[t * 288 + k], head[k], acc);
         logits[(size_t)s * kCells + t] = acc;
     }
-    if (t == 63) {      // linear 27 -> 1 + tanh
+    if (t == 64) {      // linear 27 -> 1 + tanh (a different wave than the policy lanes)
         float acc = W.vl_b[0];
         for (int k = 0; k < 27; ++k) acc = fmaf(W.vl_w[k], head[288 + k], acc);
         value[s] = tanhf(acc);
@@ -454,7 +466,7 @@ int run_search(Engine *e, uint32_t na, uint32_t sims) {
         uint32_t *cnt = e->counts.p + it;
         k_tleaf<<<na, 64, 0, e->stream>>>(view(e), bview(e), e->active.p, na, e->cfg.c, cnt, e->err.p);
         if (kind == SPAI_EVAL_NET)
-            k_tnet<<<na, 64, 0, e->stream>>>(cnt, na, e->bx.p, wview(e->net), e->blogits.p, e->bvalue.p);
+            k_tnet<<<na, kNetThreads, 0, e->stream>>>(cnt, na, e->bx.p, wview(e->net), e->blogits.p, e->bvalue.p);
         k_texpand<<<na, 64, 0, e->stream>>>(view(e), bview(e), na, cnt, kind, e->err.p);
     }
     SPAI_HIP(hipGetLastError());
@@ -807,7 +819,7 @@ int spai_ttt_net_forward(spai_ttt_net *net, uint32_t n, const float *x, float *l
         net->io_cap = n;
     }
     SPAI_HIP(hipMemcpyAsync(net->io_x.p, x, 108ull * n, hipMemcpyHostToDevice, e->stream));
-    k_tnet<<<n, 64, 0, e->stream>>>(nullptr, n, net->io_x.p, wview(net), net->io_l.p, net->io_v.p);
+    k_tnet<<<n, kNetThreads, 0, e->stream>>>(nullptr, n, net->io_x.p, wview(net), net->io_l.p, net->io_v.p);
     SPAI_HIP(hipGetLastError());
     SPAI_HIP(hipMemcpyAsync(logits, net->io_l.p, 36ull * n, hipMemcpyDeviceToHost, e->stream));
     SPAI_HIP(hipMemcpyAsync(value, net->io_v.p, 4ull * n, hipMemcpyDeviceToHost, e->stream));
@@ -833,7 +845,7 @@ int spai_ttt_predict(spai_ttt_net *net, uint32_t first, uint32_t n, float *prior
     }
     const uint32_t g = (n + 63) / 64;
     k_tslots<<<g, 64, 0, e->stream>>>(e->slots.p, first, n, 2, nullptr, nullptr, nullptr, net->io_x.p, nullptr);
-    k_tnet<<<n, 64, 0, e->stream>>>(nullptr, n, net->io_x.p, wview(net), net->io_l.p, net->io_v.p);
+    k_tnet<<<n, kNetThreads, 0, e->stream>>>(nullptr, n, net->io_x.p, wview(net), net->io_l.p, net->io_v.p);
     k_tslots<<<g, 64, 0, e->stream>>>(e->slots.p, first, n, 4, nullptr, nullptr, nullptr, e->sf2.p, net->io_l.p);
     SPAI_HIP(hipGetLastError());
     SPAI_HIP(hipMemcpyAsync(priors, e->sf2.p, 36ull * n, hipMemcpyDeviceToHost, e->stream));
