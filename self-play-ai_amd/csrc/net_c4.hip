@@ -215,8 +215,14 @@ __device__ __forceinline__ void make_geo(int lane, Geo<Plan<W, CT, NPT>::NT> &g)
 // hide a weight load (L2) or an LDS read behind, but registers to spare.
 // (DA must divide the 18 k-steps of a layer: the ring carries the next layer's
 // first DA-1 k-steps in the slots a fresh layer expects.)
-__host__ __device__ constexpr int a_depth(int S) { return S <= 2 ? 9 : S <= 4 ? 6 : 3; }
-__host__ __device__ constexpr int b_depth(int S) { return S <= 2 ? 4 : S <= 3 ? 3 : 2; }
+#ifndef SPAI_DA4
+#define SPAI_DA4 6   // A ring at S = 4 (tuning knob)
+#endif
+#ifndef SPAI_DB4
+#define SPAI_DB4 2   // B ring at S = 4 (tuning knob)
+#endif
+__host__ __device__ constexpr int a_depth(int S) { return S <= 2 ? 9 : S <= 3 ? 6 : S <= 4 ? SPAI_DA4 : 3; }
+__host__ __device__ constexpr int b_depth(int S) { return S <= 2 ? 4 : S <= 3 ? 3 : S <= 4 ? SPAI_DB4 : 2; }
 
 // implicit-GEMM 3x3 conv over the LDS activations at IN for wave W's tasks.
 // Software pipeline: A (weights, global/L2) DA-1 k-steps ahead, B (LDS) DB-1
