@@ -10,7 +10,7 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
   rm -rf /tmp/pmc$i
-  timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d /tmp/pmc$i -o p -- python3 scripts/net_forward_bench.py 4096 10 > gpurun_out/pmc_$TAG/run$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d /tmp/pmc$i -o p -- python3 scripts/net_forward_bench.py ${FWD_N:-4096} ${FWD_REPS:-10} > gpurun_out/pmc_$TAG/run$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"
   find /tmp/pmc$i -name '*counter_collection*.csv' -exec cp {} gpurun_out/pmc_$TAG/pass$i.csv \;
   [ $rc -eq 0 ] || exit $rc
