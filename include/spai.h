@@ -398,6 +398,10 @@ int spai_chess_trees_create(spai_chess *e, uint32_t n);                   /* n x
 int spai_chess_search(spai_chess *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_searches, float *policy,
                       uint32_t *child_ids, float *child_visits, uint16_t *child_moves, uint32_t *n_children);
 /* Tree::use_subtree for the k-th root child (k in [0, n_children)); the new root keeps N and W */
+/* Tree::with_root_state (mcts.rs:86-89): tree `tree` becomes a one-node tree rooted at the
+ * state held in game slot `slot` (board, MakeMove count, fifty-move counter and the slot's
+ * history of earlier positions, which the repetition rule reads) */
+int spai_chess_tree_reset(spai_chess *e, uint32_t tree, uint32_t slot);
 int spai_chess_tree_use_subtree(spai_chess *e, uint32_t tree, uint32_t child_index);
 int spai_chess_tree_root(spai_chess *e, uint32_t tree, spai_chess_state *root, uint32_t *visits, float *value_sum);
 /* use_subtree for n trees at once (child_index[i] of tree_idx[i]'s root children); status[i] /
@@ -453,6 +457,8 @@ int spai_ttt_trees_create(spai_ttt *e, uint32_t n);
 /* per tree i: policy [i][9], child_ids / child_visits [i][9], n_children [i] (any may be NULL) */
 int spai_ttt_search(spai_ttt *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_searches, float *policy,
                     uint32_t *child_ids, float *child_visits, uint32_t *n_children);
+/* Tree::with_root_state (mcts.rs:86-89) */
+int spai_ttt_tree_reset(spai_ttt *e, uint32_t tree, const spai_ttt_state *root);
 int spai_ttt_tree_use_subtree(spai_ttt *e, uint32_t tree, uint32_t child_index);
 /* SelfPlayWorker::self_play; the sink gets encodings [n][27], policies [n][9], values, moves */
 int spai_ttt_selfplay_run(spai_ttt *e, uint32_t n_games, uint64_t game_id_base, spai_sample_sink sink, void *user,

@@ -638,6 +638,14 @@ orc_tree *orc_tree_create(void) {
     return t;
 }
 
+/* Tree::with_root_state (mcts.rs:86-89): one root node holding a copy of s
+ * (the transposition table is a persistent list, so the copy shares it) */
+orc_tree *orc_tree_with_root(const orc_state *s) {
+    orc_tree *t = orc_tree_create();
+    t->arena[0].state = *s;
+    return t;
+}
+
 void orc_tree_destroy(orc_tree *t) {
     if (!t) return;
     for (int i = 0; i < t->size; ++i) free(t->arena[i].children);

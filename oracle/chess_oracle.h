@@ -100,6 +100,7 @@ void orc_hash_eval_raw(const orc_state *s, float *raw, float *value);
 /* ---- MCTS over chess trees (mcts.rs), full State per node ---- */
 typedef struct orc_tree orc_tree;
 orc_tree *orc_tree_create(void);
+orc_tree *orc_tree_with_root(const orc_state *s);   /* Tree::with_root_state */
 void orc_tree_destroy(orc_tree *t);
 void orc_tree_use_subtree(orc_tree *t, int new_root_id);
 const orc_state *orc_tree_node_state(const orc_tree *t, int id);

@@ -62,6 +62,8 @@ def lib():
         L.orc_position_key.argtypes = [vp]
         L.orc_hash_eval_raw.argtypes = [vp, fp, fp]
         L.orc_tree_create.restype = vp
+        L.orc_tree_with_root.restype = vp
+        L.orc_tree_with_root.argtypes = [C.POINTER(State)]
         L.orc_tree_destroy.argtypes = [vp]
         L.orc_tree_use_subtree.argtypes = [vp, i]
         L.orc_tree_node_state.restype = C.POINTER(State)
@@ -191,10 +193,15 @@ def arena_reset():
     lib().orc_arena_reset()
 
 
-def search(n_trees, num_searches, c=2.0):
-    """Mcts::search with the hash stub over n fresh trees from the start position."""
+def search(n_trees, num_searches, c=2.0, states=None):
+    """Mcts::search with the hash stub over n fresh trees from the start position,
+    or (states = list of ChessState) over Tree::with_root_state(state) trees."""
     L = lib()
-    trees = [L.orc_tree_create() for _ in range(n_trees)]
+    if states is not None:
+        n_trees = len(states)
+        trees = [L.orc_tree_with_root(C.byref(st.st)) for st in states]
+    else:
+        trees = [L.orc_tree_create() for _ in range(n_trees)]
     arr = (C.c_void_p * n_trees)(*trees)
     pol = np.zeros((n_trees, POLICY), np.float32)
     ids = np.zeros((n_trees, MAX_MOVES), np.int32)

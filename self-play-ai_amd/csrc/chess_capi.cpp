@@ -274,6 +274,11 @@ int spai_chess_search(spai_chess *e, uint32_t n, const uint32_t *tree_idx, uint3
     return search(e, n, tree_idx, num_searches, policy, child_ids, child_visits, child_moves, n_children, nullptr);
 }
 
+int spai_chess_tree_reset(spai_chess *e, uint32_t tree, uint32_t slot) {
+    CH_CHECK(e);
+    return tree_reset_from_slot(e, tree, slot);
+}
+
 int spai_chess_tree_use_subtree(spai_chess *e, uint32_t tree, uint32_t child_index) {
     CH_CHECK(e);
     return tree_use_subtree(e, tree, child_index);

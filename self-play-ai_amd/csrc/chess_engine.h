@@ -134,6 +134,7 @@ int trees_create(spai_chess *e, uint32_t n);
 int search(spai_chess *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_searches, float *policy,
            uint32_t *child_ids, float *child_visits, uint16_t *child_moves, uint32_t *n_children, double *evals);
 int tree_use_subtree(spai_chess *e, uint32_t tree, uint32_t child_index);
+int tree_reset_from_slot(spai_chess *e, uint32_t tree, uint32_t slot);
 int tree_root(spai_chess *e, uint32_t tree, spai_chess_state *root, uint32_t *visits, float *value_sum);
 int trees_advance(spai_chess *e, uint32_t n, const uint32_t *tree_idx, const uint32_t *child_index, uint8_t *status,
                   uint32_t *reps);

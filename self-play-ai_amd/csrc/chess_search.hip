@@ -362,6 +362,50 @@ __global__ void k_ctrees_init(TV T, uint32_t n) {
     T.hist_n[t] = 0;
 }
 
+// Tree::with_root_state (mcts.rs:86-89) for the state held in game slot `slot`:
+// a one-node tree whose root is that board, with the slot's history of earlier
+// positions (their move-list hashes) as the tree's, and its repetition count and
+// status.  One wave.
+__global__ void k_ctree_from_slot(TV T, uint32_t t, const Board *__restrict__ boards,
+                                  const uint64_t *__restrict__ shist, const uint32_t *__restrict__ sn_hist,
+                                  uint32_t smax_hist, uint32_t slot, uint32_t *err) {
+    const int lane = threadIdx.x;
+    Board b = boards[slot];
+    const uint32_t nh = sn_hist[slot];
+    if (nh > T.max_hist) {
+        if (lane == 0) atomicOr(err, kErrHist);
+        return;
+    }
+    const uint64_t *src = shist + (size_t)slot * smax_hist;
+    uint64_t *dst = T.hist + (size_t)t * T.max_hist;
+    const GenOut g = wave_movegen(b, nullptr, lane);
+    uint32_t hits = 0;
+    for (uint32_t i = lane; i < nh; i += 64) {
+        const uint64_t h = src[i];
+        dst[i] = h;
+        hits += h == g.hash;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) hits += __shfl_xor(hits, o, 64);
+    const uint32_t reps = 1 + hits;
+    int status = SPAI_ONGOING;
+    if (g.n == 0) status = g.in_check ? SPAI_WON : SPAI_TIED;
+    else if (reps >= 3 || b.fifty >= 100) status = SPAI_TIED;
+    b.status = (uint8_t)status;
+    if (lane == 0) {
+        const size_t base = (size_t)t * 2 * T.cap;
+        T.nodes[base] = make_uint4(0u, 0u, 0u, 0u);
+        T.first[base] = kNone;
+        T.nhash[base] = 0;
+        T.root[t] = 0;
+        T.fill[t] = 1;
+        T.half[t] = 0;
+        T.root_board[t] = b;
+        T.root_reps[t] = reps;
+        T.hist_n[t] = nh;
+    }
+}
+
 // root children after a search (mcts.rs:310-331): n_children, visits, moves, ids
 __global__ void k_croot_stats(TV T, const uint32_t *__restrict__ active, uint32_t n_active, uint32_t *nch_out,
                               uint32_t *vis_out, uint16_t *mv_out, uint32_t *id_out) {
@@ -664,6 +708,16 @@ int search(spai_chess *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_sea
         if (policy) dense_policy(rb[tree_idx[i]].side, nch, vis, mv, policy + (size_t)i * kPolicy);
     }
     return SPAI_OK;
+}
+
+int tree_reset_from_slot(spai_chess *e, uint32_t tree, uint32_t slot) {
+    Trees &Tr = e->trees;
+    SPAI_CHECK(tree < Tr.n, SPAI_ERR_INVALID, "tree %u out of range (%u trees)", tree, Tr.n);
+    SPAI_CHECK(slot < e->slots.n, SPAI_ERR_INVALID, "slot %u out of range (%u slots)", slot, e->slots.n);
+    k_ctree_from_slot<<<1, 64, 0, e->stream>>>(view(e), tree, e->slots.board.p, e->slots.hist.p, e->slots.n_hist.p,
+                                               e->slots.max_hist, slot, e->err.p);
+    SPAI_HIP(hipGetLastError());
+    return check_err(e);
 }
 
 int tree_use_subtree(spai_chess *e, uint32_t tree, uint32_t child_index) {

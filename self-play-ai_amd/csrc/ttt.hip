@@ -376,6 +376,14 @@ __global__ void k_ttrees_init(TV T, uint32_t n) {
     T.root_state[t] = State{0, 0, 0, 0};
 }
 
+// Tree::with_root_state (mcts.rs:86-89): tree t becomes a one-node tree rooted at s
+__global__ void k_ttree_reset(TV T, uint32_t t, State s) {
+    T.nodes[(size_t)t * T.cap] = make_uint4(0u, 0u, 0u, kNoChildren);
+    T.root[t] = 0;
+    T.next_free[t] = 1;
+    T.root_state[t] = s;
+}
+
 __global__ void k_tadvance(TV T, const uint32_t *__restrict__ active, uint32_t n_active,
                            const uint32_t *__restrict__ pick, State *out) {
     const uint32_t gi = blockIdx.x * blockDim.x + threadIdx.x;
@@ -885,6 +893,19 @@ int spai_ttt_search(spai_ttt *e, uint32_t n, const uint32_t *tree_idx, uint32_t 
                      child_ids ? child_ids + 9 * i : nullptr, child_visits ? child_visits + 9 * i : nullptr);
         if (n_children) n_children[i] = st[11 * i];
     }
+    return SPAI_OK;
+}
+
+int spai_ttt_tree_reset(spai_ttt *e, uint32_t tree, const spai_ttt_state *root) {
+    T_CHECK(e);
+    T_PTR(root);
+    SPAI_CHECK(tree < e->n_trees, SPAI_ERR_INVALID, "tree %u out of range (%u trees)", tree, e->n_trees);
+    const State st = ttt_from_abi(*root);
+    SPAI_CHECK(!(st.x & st.o) && st.x <= kFull && st.o <= kFull && st.status <= SPAI_WON, SPAI_ERR_INVALID,
+               "bad TicTacToe state");
+    k_ttree_reset<<<1, 1, 0, e->stream>>>(view(e), tree, st);
+    SPAI_HIP(hipGetLastError());
+    SPAI_HIP(hipStreamSynchronize(e->stream));
     return SPAI_OK;
 }
 

@@ -54,6 +54,7 @@ def lib():
         L.spai_chess_net_forward.argtypes = [vp, u32, vp, vp, vp]
         L.spai_chess_predict.argtypes = [vp, u32, u32, vp, vp]
         L.spai_chess_rules_bench.argtypes = [vp, u32, u32, u32, vp]
+        L.spai_chess_tree_reset.argtypes = [vp, u32, u32]
         L.spai_chess_set_net.argtypes = [vp, vp]
         L.spai_chess_trees_create.argtypes = [vp, u32]
         L.spai_chess_search.argtypes = [vp, u32, vp, u32, vp, vp, vp, vp, vp]
@@ -212,6 +213,10 @@ class ChessEngine:
         ns = self.cfg.num_searches if num_searches is None else num_searches
         _check(lib().spai_chess_search(self.h, n, _p(idx), ns, _p(pol), _p(ids), _p(vis), _p(mv), _p(nc)))
         return pol, ids, vis, mv, nc
+
+    def tree_reset(self, tree, slot):
+        """Tree::with_root_state(state of game slot `slot`)"""
+        _check(lib().spai_chess_tree_reset(self.h, tree, slot))
 
     def use_subtree(self, tree, child_index):
         _check(lib().spai_chess_tree_use_subtree(self.h, tree, child_index))

@@ -38,6 +38,7 @@ def lib():
         L.spai_ttt_trees_create.argtypes = [vp, u32]
         L.spai_ttt_search.argtypes = [vp, u32, vp, u32, vp, vp, vp, vp]
         L.spai_ttt_tree_use_subtree.argtypes = [vp, u32, u32]
+        L.spai_ttt_tree_reset.argtypes = [vp, u32, vp]
         L.spai_ttt_selfplay_run.argtypes = [vp, u32, u64, SINK, vp, P(SelfPlayStats)]
         _ready = True
     return L
@@ -140,6 +141,11 @@ class TTTEngine:
         ns = self.cfg.num_searches if num_searches is None else num_searches
         _check(lib().spai_ttt_search(self.h, n, _p(idx), ns, _p(pol), _p(ids), _p(vis), _p(nc)))
         return pol, ids, vis, nc
+
+    def tree_reset(self, tree, state):
+        """Tree::with_root_state(state); state = one STATE_DTYPE record"""
+        a = np.ascontiguousarray(np.asarray(state, STATE_DTYPE).reshape(1))
+        _check(lib().spai_ttt_tree_reset(self.h, tree, _p(a)))
 
     def use_subtree(self, tree, child_index):
         _check(lib().spai_ttt_tree_use_subtree(self.h, tree, child_index))

@@ -308,3 +308,51 @@ def test_chess_self_play_net_legal(ch, sc):
         assert np.allclose(g["policy"].sum(1), 1.0, atol=1e-5)
     ch.arena_reset()
     eng.close()
+
+
+def test_chess_tree_reset_from_slot_matches_oracle(ch, sc):
+    """Tree::with_root_state from game slots: random games and a knight shuffle
+    whose root has already occurred once (the search meets threefold repetition
+    through the copied history); visit counts bit-exact vs the oracle (hash stub)."""
+    rng = random.Random(17)
+    shuffle = [ch.move(ch.sq(a), ch.sq(b)) for a, b in
+               [("g1", "f3"), ("g8", "f6"), ("f3", "g1"), ("f6", "g8"), ("g1", "f3"), ("g8", "f6")]]
+    seqs = [shuffle]
+    for g in range(5):
+        s, seq = ch.ChessState(), []
+        for _ in range(rng.randrange(1, 40)):
+            mv = s.valid_actions()
+            if not mv or s.status:
+                break
+            m = rng.choice(mv)
+            seq.append(m)
+            s = s.next_state(m)
+        seqs.append(seq)
+    n, sims = len(seqs), 48
+    states = []
+    eng = sc.ChessEngine(num_searches=sims, max_trees=n, eval_kind=sc.EVAL_HASH)
+    eng.games_resize(n)
+    for p in range(max(len(q) for q in seqs)):
+        eng.apply(np.array([q[p] if p < len(q) else 0 for q in seqs], np.uint16), check=False)
+    for q in seqs:
+        s = ch.ChessState()
+        for m in q:
+            s = s.next_state(m)
+        states.append(s)
+    live = [i for i, s in enumerate(states) if not s.status]
+    eng.trees_create(n)
+    for t, i in enumerate(live):
+        eng.tree_reset(t, i)
+    pol, ids, vis, mv, nc = eng.search(np.arange(len(live)))
+    rc, rpol, rids, rvis, rmv, rnc = ch.search(0, sims, states=[states[i] for i in live])
+    assert rc >= 0
+    assert np.array_equal(nc, rnc)
+    for t in range(len(live)):
+        k = nc[t]
+        assert np.array_equal(vis[t, :k], rvis[t, :k]), t
+        assert np.array_equal(mv[t, :k], rmv[t, :k].astype(np.uint16)), t
+    assert np.array_equal(pol, rpol)
+    with pytest.raises(sc.SpaiError):
+        eng.tree_reset(0, n)          # slot out of range
+    ch.arena_reset()
+    eng.close()

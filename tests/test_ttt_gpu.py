@@ -174,3 +174,45 @@ def test_ttt_config1_self_play_with_net(oracle, st):
     assert np.array_equal(g["value"], np.array(exp, np.float32))
     assert np.allclose(g["policy"].sum(1), 1.0, atol=1e-6)
     eng.close()
+
+
+def test_ttt_tree_reset_matches_oracle(oracle, st):
+    """Tree::with_root_state from arbitrary positions, hash-stub search bit-exact vs the oracle"""
+    rng = random.Random(8)
+    roots = []
+    for _ in range(12):
+        g = oracle.TTT()
+        for _ in range(rng.randrange(0, 6)):
+            empty = [r * 3 + c for r in range(3) for c in range(3) if g.st.board[r][c] == 0]
+            if g.status or not empty:
+                break
+            g = g.next_state(rng.choice(empty))
+        if g.status == 0:
+            roots.append(g)
+    n, sims = len(roots), 40
+    eng = st.TTTEngine(num_searches=sims, max_trees=n, eval_kind=st.EVAL_HASH)
+    eng.trees_create(n)
+    for i, g in enumerate(roots):
+        x, o = _bits(g)
+        rec = np.zeros(1, st.STATE_DTYPE)
+        rec["x"], rec["o"], rec["n"], rec["status"] = x, o, g.st.num_actions_played, g.status
+        eng.tree_reset(i, rec)
+    pol, ids, vis, nc = eng.search(np.arange(n))
+    L = oracle.lib()
+    trees = [L.or_tree_with_root(oracle.GAME_TICTACTOE, C.byref(g.st)) for g in roots]
+    arr = (C.c_void_p * n)(*trees)
+    rpol = np.zeros((n, 9), np.float32)
+    rids = np.zeros((n, 9), np.int32)
+    rvis = np.zeros((n, 9), np.float32)
+    rnc = np.zeros(n, np.int32)
+    rc = L.or_search(arr, n, sims, 2.0, oracle.EVAL_HASH, None, oracle.EVAL_FN(), None, oracle._f(rpol),
+                     oracle._i(rids), oracle._f(rvis), oracle._i(rnc))
+    for t in trees:
+        L.or_tree_destroy(t)
+    assert rc >= 0
+    assert np.array_equal(nc, rnc) and np.array_equal(vis, rvis) and np.array_equal(pol, rpol)
+    bad = np.zeros(1, st.STATE_DTYPE)
+    bad["x"], bad["o"] = 1, 1
+    with pytest.raises(st.SpaiError):
+        eng.tree_reset(0, bad)
+    eng.close()
