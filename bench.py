@@ -43,6 +43,13 @@ def flops_per_eval(blocks, hid=64):
     return conv(3, hid) + 2 * blocks * conv(hid, hid) + conv(hid, 32) + conv(hid, 3) + 2 * 1344 * 7 + 2 * 126
 
 
+def weight_bytes(blocks):
+    """bytes the fused C4 forward reads as weights (net_c4.hip packing): residual convs
+    [2*blocks][18 k-steps][4 co tiles] x 1 KiB fragments, stem 4 KiB, head [18][3] x 1 KiB,
+    fused linear 48 x 1 KiB, fp32 biases (64 + 2*blocks*64 + 48) + 8"""
+    return 2 * blocks * 18 * 4 * 1024 + 4096 + 18 * 3 * 1024 + 48 * 1024 + 4 * (64 + 2 * blocks * 64 + 48 + 8)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -293,6 +300,9 @@ def main():
                      "achieved": achieved, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / BF16_PEAK_TFLOPS if achieved else None, "traffic": traffic,
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                     # algorithmic bytes of one launch: the packed bf16 weights + fp32 biases once,
+                     # plus per leaf 16 B of bitboards in and 36 B (8 priors + value) out
+                     "algorithmic_bytes": weight_bytes(args.blocks) + 52 * (ev["items"] / max(1, ev["launches"])),
                      "flop_per_launch": per_launch_flop, "flop_per_eval": fpe,
                      # whole-GPU view: every forward FLOP of the timed region over its wall time
                      # (the two search chains' forwards overlap, so this is not per launch)
