@@ -36,6 +36,15 @@ def flops_per_eval(blocks):
             conv(256, 1, 1) + 2 * 64 * 256 + 2 * 256)
 
 
+def weight_bytes(blocks):
+    """bytes k_chess_forward reads as weights (chess_net.hip packing): bf16 conv fragments
+    (stem 32 padded input channels, 2*blocks residual 3x3 convs, policy 1x1 256->256 and
+    256->80 padded), fp32 biases and the fp32 value head (1x1 256->1, linear 64->256, 256->1)"""
+    bf16 = 32 * 256 * 9 + 2 * blocks * 256 * 256 * 9 + 256 * 256 + 256 * 80
+    f32 = 256 + 2 * blocks * 256 + 256 + 80 + (256 + 1) + (64 * 256 + 256) + (256 + 1)
+    return 2 * bf16 + 4 * f32
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--games", type=int, default=1024)
@@ -210,7 +219,9 @@ def main():
                      "achieved": achieved, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / BF16_PEAK_TFLOPS if achieved else None, "traffic": traffic,
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
-                     "flop_per_eval": fpe, "avg_leaves_per_launch": leaves, "avg_launch_ms": ms[1]},
+                     "flop_per_eval": fpe, "avg_leaves_per_launch": leaves, "avg_launch_ms": ms[1],
+                     # weights once + per leaf the bf16 input planes [64][32] in, 4672 logits + value out
+                     "algorithmic_bytes": weight_bytes(args.blocks) + leaves * (64 * 32 * 2 + 4672 * 4 + 4)},
     }
     net.close()
     eng.close()
