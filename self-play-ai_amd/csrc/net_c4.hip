@@ -146,9 +146,14 @@ __device__ __forceinline__ uint32_t pack_relu_bf16x2(float a, float b) {
 #ifndef SPAI_PAIR_MAX_NPT
 #define SPAI_PAIR_MAX_NPT 11
 #endif
+#ifndef SPAI_HEAD_CO_MAJOR_MAX_NPT
+#define SPAI_HEAD_CO_MAJOR_MAX_NPT 8   // the head conv (CT = 3) in co-major order up to this many tiles
+#endif
 template <int W, int CT, int NPT>
 struct Plan {
-    static constexpr int MODE = NPT <= SPAI_CO_MAJOR_MAX_NPT ? 1 : CT == 4 && NPT <= SPAI_PAIR_MAX_NPT ? 2 : 0;
+    static constexpr int MODE = NPT <= (CT == 3 ? SPAI_HEAD_CO_MAJOR_MAX_NPT : SPAI_CO_MAJOR_MAX_NPT) ? 1
+                                : CT == 4 && NPT <= SPAI_PAIR_MAX_NPT                              ? 2
+                                                                                                    : 0;
     static constexpr int TT = NPT * CT;
     // position-major / co-major: a contiguous task range
     static constexpr int first = TT * W / 4;
