@@ -189,9 +189,9 @@ int spai_selfplay_run(spai_engine *eng, uint32_t n_games, uint64_t game_id_base,
 
 /* ------------------------------------------------------------------ profiling
  * Per-kernel average device time of the last spai_selfplay_run / spai_search
- * call, measured with HIP events on the engine stream when enabled.  enabled = 1
- * samples every 4th search iteration of chain 0; enabled = k > 1 every k-th
- * (each sampled iteration adds six event records to the stream). */
+ * call, measured with HIP events on each search chain's stream when enabled.
+ * enabled = 1 samples every 4th search iteration; enabled = k > 1 every k-th
+ * (each sampled iteration adds six event records per chain). */
 int spai_engine_set_timing(spai_engine *eng, int enabled);
 /* ms[0] select, ms[1] evaluate (NN forward), ms[2] expand+backup; launches[3] */
 int spai_engine_timing(spai_engine *eng, double *avg_ms, double *launches);
