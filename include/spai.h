@@ -255,8 +255,9 @@ int spai_learner_set_comm(spai_learner *l, int rank, int world, const uint8_t *i
  * safetensors files with tch VarStore naming (VarStore::save / load,
  * learner.rs:192, main.rs:61): the flat construction-order parameters <-> one
  * F32 tensor per variable ("weight", "bias", "weight__2", ... "running_var__5"
- * ...), shapes as tch (conv [co][ci][3][3], linear [out][in]).  Host-only: no
- * device needed. */
+ * ...), shapes as tch (conv [co][ci][k][k], linear [out][in]).  game = Connect4,
+ * TicTacToe (hidden 64) or chess (hidden 256; the flat layout of
+ * spai_chess_net_init_params).  Host-only: no device needed. */
 int spai_params_save_safetensors(int game, int blocks, int hidden, const float *params, size_t n_params,
                                  const char *path);
 int spai_params_load_safetensors(int game, int blocks, int hidden, const char *path, float *params,

@@ -4,7 +4,8 @@
 // (learner.rs:192, learner_concurrent.rs:155-156, main.rs:61).  tch 0.13 keys
 // every variable by its path name on the root path; a name already present
 // gets the suffix "__<number of variables in the store>" (nn::Path::add).
-// Construction order (model/mod.rs:167-184, model/connect_four.rs:54-72):
+// Construction order (model/mod.rs:167-184, model/connect_four.rs:54-72,
+// model/tictactoe.rs:54-72, model/chess.rs:48-70):
 // each conv2d adds weight, bias; each batch_norm2d weight, bias, running_mean,
 // running_var; each linear weight, bias — stem, residual blocks, policy head,
 // value head.  tch is not vendored: this naming is restated from its source as
@@ -32,12 +33,12 @@ struct TensorSpec {
     size_t count;
 };
 
-// the C4 net's variables in construction order, with tch names and shapes
-std::vector<TensorSpec> c4_specs(int blocks, int hidden) {
+// A net's variables in construction order, with tch names and shapes.
+struct SpecBuilder {
     std::vector<TensorSpec> out;
     std::map<std::string, int> seen;
     size_t off = 0;
-    auto add = [&](const std::string &base, std::vector<int64_t> shape) {
+    void add(const std::string &base, std::vector<int64_t> shape) {
         size_t n = 1;
         for (int64_t d : shape) n *= (size_t)d;
         std::string name = base;
@@ -45,25 +46,53 @@ std::vector<TensorSpec> c4_specs(int blocks, int hidden) {
         seen[base] = 1;
         out.push_back({name, shape, off, n});
         off += n;
-    };
-    auto conv_bn = [&](int64_t ci, int64_t co) {
-        add("weight", {co, ci, 3, 3});
+    }
+    void conv(int64_t ci, int64_t co, int64_t k) {   // nn::conv2d: weight, bias
+        add("weight", {co, ci, k, k});
         add("bias", {co});
-        add("weight", {co});
-        add("bias", {co});
-        add("running_mean", {co});
-        add("running_var", {co});
-    };
-    conv_bn(3, hidden);
-    for (int b = 0; b < 2 * blocks; ++b) conv_bn(hidden, hidden);
-    conv_bn(hidden, 32);
-    add("weight", {7, 32 * 42});
-    add("bias", {7});
-    conv_bn(hidden, 3);
-    add("weight", {1, 3 * 42});
-    add("bias", {1});
-    return out;
+    }
+    void bn(int64_t c) {                              // nn::batch_norm2d
+        add("weight", {c});
+        add("bias", {c});
+        add("running_mean", {c});
+        add("running_var", {c});
+    }
+    void conv_bn(int64_t ci, int64_t co) {
+        conv(ci, co, 3);
+        bn(co);
+    }
+    void linear(int64_t in, int64_t outf) {           // nn::linear: weight [out][in], bias
+        add("weight", {outf, in});
+        add("bias", {outf});
+    }
+};
+
+// Connect4 (model/connect_four.rs:50-72) and TicTacToe (model/tictactoe.rs:50-72):
+// torso (model/mod.rs:167-184), policy head conv 32 + linear, value head conv 3 + linear
+// chess (model/chess.rs:48-70): torso, policy head 1x1 convs (no BN), value head 1x1 conv + 2 linears
+std::vector<TensorSpec> net_specs(int game, int blocks, int hidden) {
+    SpecBuilder b;
+    if (game == SPAI_GAME_CHESS) {
+        b.conv_bn(19, hidden);
+        for (int i = 0; i < 2 * blocks; ++i) b.conv_bn(hidden, hidden);
+        b.conv(hidden, 256, 1);
+        b.conv(256, 73, 1);
+        b.conv(hidden, 1, 1);
+        b.linear(64, 256);
+        b.linear(256, 1);
+        return b.out;
+    }
+    const int64_t cells = game == SPAI_GAME_TICTACTOE ? 9 : 42, actions = game == SPAI_GAME_TICTACTOE ? 9 : 7;
+    b.conv_bn(3, hidden);
+    for (int i = 0; i < 2 * blocks; ++i) b.conv_bn(hidden, hidden);
+    b.conv_bn(hidden, 32);
+    b.linear(32 * cells, actions);
+    b.conv_bn(hidden, 3);
+    b.linear(3 * cells, 1);
+    return b.out;
 }
+
+size_t specs_total(const std::vector<TensorSpec> &v) { return v.empty() ? 0 : v.back().offset + v.back().count; }
 
 // ---- a minimal JSON reader for the safetensors header (objects, strings, integer arrays)
 struct Json {
@@ -158,10 +187,10 @@ struct Entry {
 }  // namespace
 
 int params_save_safetensors(int game, int blocks, int hidden, const float *params, size_t n, const char *path) {
-    SPAI_CHECK(game == SPAI_GAME_CONNECT4, SPAI_ERR_UNSUPPORTED, "safetensors: only the Connect4 net is built");
-    SPAI_CHECK(n == net_num_params(game, blocks, hidden), SPAI_ERR_INVALID, "expected %zu params, got %zu",
-               net_num_params(game, blocks, hidden), n);
-    const std::vector<TensorSpec> specs = c4_specs(blocks, hidden);
+    SPAI_CHECK(game >= SPAI_GAME_TICTACTOE && game <= SPAI_GAME_CHESS, SPAI_ERR_INVALID, "bad game %d", game);
+    SPAI_CHECK(blocks >= 0 && hidden > 0, SPAI_ERR_INVALID, "bad net shape");
+    const std::vector<TensorSpec> specs = net_specs(game, blocks, hidden);
+    SPAI_CHECK(n == specs_total(specs), SPAI_ERR_INVALID, "expected %zu params, got %zu", specs_total(specs), n);
     std::string h = "{\"__metadata__\":{\"format\":\"pt\"}";
     size_t byte = 0;
     for (const TensorSpec &t : specs) {
@@ -186,9 +215,10 @@ int params_save_safetensors(int game, int blocks, int hidden, const float *param
 }
 
 int params_load_safetensors(int game, int blocks, int hidden, const char *path, float *params, size_t n) {
-    SPAI_CHECK(game == SPAI_GAME_CONNECT4, SPAI_ERR_UNSUPPORTED, "safetensors: only the Connect4 net is built");
-    SPAI_CHECK(n == net_num_params(game, blocks, hidden), SPAI_ERR_INVALID, "expected %zu params, got %zu",
-               net_num_params(game, blocks, hidden), n);
+    SPAI_CHECK(game >= SPAI_GAME_TICTACTOE && game <= SPAI_GAME_CHESS, SPAI_ERR_INVALID, "bad game %d", game);
+    SPAI_CHECK(blocks >= 0 && hidden > 0, SPAI_ERR_INVALID, "bad net shape");
+    const std::vector<TensorSpec> specs = net_specs(game, blocks, hidden);
+    SPAI_CHECK(n == specs_total(specs), SPAI_ERR_INVALID, "expected %zu params, got %zu", specs_total(specs), n);
     FILE *f = std::fopen(path, "rb");
     SPAI_CHECK(f, SPAI_ERR_INVALID, "cannot open %s", path);
     std::vector<uint8_t> buf;
@@ -236,7 +266,7 @@ int params_load_safetensors(int game, int blocks, int hidden, const char *path, 
         } while (js.ok && js.eat(','));
         SPAI_CHECK(js.ok && js.eat('}'), SPAI_ERR_INVALID, "%s: bad header", path);
     }
-    for (const TensorSpec &t : c4_specs(blocks, hidden)) {
+    for (const TensorSpec &t : specs) {
         auto it = entries.find(t.name);
         SPAI_CHECK(it != entries.end(), SPAI_ERR_INVALID, "%s: missing tensor '%s'", path, t.name.c_str());
         const Entry &e = it->second;

@@ -470,9 +470,10 @@ def save_params(path, params, blocks, hidden=64, game=GAME_CONNECT4):
     _check(lib().spai_params_save_safetensors(game, blocks, hidden, _p(p), len(p), os.fsencode(path)))
 
 
-def load_params(path, blocks, hidden=64, game=GAME_CONNECT4):
-    """safetensors with tch VarStore names -> flat parameters (VarStore::load)"""
-    out = np.zeros(num_params(blocks, hidden, game), np.float32)
+def load_params(path, blocks, hidden=64, game=GAME_CONNECT4, n=None):
+    """safetensors with tch VarStore names -> flat parameters (VarStore::load).
+    n: parameter count for the TicTacToe / chess nets (spai_ttt.num_params, spai_chess.num_params)"""
+    out = np.zeros(num_params(blocks, hidden, game) if n is None else n, np.float32)
     _check(lib().spai_params_load_safetensors(game, blocks, hidden, os.fsencode(path), _p(out), len(out)))
     return out
 

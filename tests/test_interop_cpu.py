@@ -86,3 +86,41 @@ def test_safetensors_errors(tmp_path):
         spai.load_params(bad, blocks)
     with pytest.raises(spai.SpaiError):
         spai.load_params(str(tmp_path / "missing.safetensors"), blocks)
+
+
+
+def test_safetensors_ttt_and_chess_nets(tmp_path):
+    """the TicTacToe (model/tictactoe.rs) and chess (model/chess.rs) nets: round trip, and the
+    official reader sees tch names/shapes whose construction-order concatenation is the flat vector"""
+    import spai_chess
+    import spai_ttt
+    p = spai_ttt.init_params(2, 4)
+    path = str(tmp_path / "ttt.safetensors")
+    spai.save_params(path, p, 2, game=spai.GAME_TICTACTOE)
+    np.testing.assert_array_equal(spai.load_params(path, 2, game=spai.GAME_TICTACTOE, n=p.size), p)
+    t = st.load_file(path)
+    names = expected_names(2)
+    assert set(t) == set(names)
+    np.testing.assert_array_equal(np.concatenate([t[n].reshape(-1) for n in names]), p)
+    assert t["weight"].shape == (64, 3, 3, 3) and t[names[-2]].shape == (1, 27)
+    assert t[names[-2 - 6 - 2]].shape == (9, 288)
+
+    blocks = 1
+    p = spai_chess.init_params(blocks, 2)
+    path = str(tmp_path / "chess.safetensors")
+    spai.save_params(path, p, blocks, hidden=256, game=spai.GAME_CHESS)
+    np.testing.assert_array_equal(spai.load_params(path, blocks, hidden=256, game=spai.GAME_CHESS, n=p.size), p)
+    t = st.load_file(path)
+    names, seen = [], set()
+    for base in (["weight", "bias", "weight", "bias", "running_mean", "running_var"] * (1 + 2 * blocks) +
+                 ["weight", "bias"] * 5):
+        names.append(base + "__%d" % len(names) if base in seen else base)
+        seen.add(base)
+    assert set(t) == set(names)
+    np.testing.assert_array_equal(np.concatenate([t[n].reshape(-1) for n in names]), p)
+    shapes = [t[n].shape for n in names]
+    assert shapes[0] == (256, 19, 3, 3)
+    assert shapes[-10:] == [(256, 256, 1, 1), (256,), (73, 256, 1, 1), (73,), (1, 256, 1, 1), (1,),
+                            (256, 64), (256,), (1, 256), (1,)]
+    with pytest.raises(spai.SpaiError):      # wrong count for the architecture
+        spai.save_params(path, p[:-1], blocks, hidden=256, game=spai.GAME_CHESS)
