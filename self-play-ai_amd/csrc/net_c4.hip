@@ -618,6 +618,9 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
     const int ngroups = (int)((count + S - 1) / S);
     if ((int)blockIdx.x >= ngroups) return;
     const int tid = threadIdx.x, lane = tid & 63;
+#ifdef SPAI_FWD_PRIO
+    __builtin_amdgcn_s_setprio(SPAI_FWD_PRIO);   // experiment: issue priority against co-resident tree kernels
+#endif
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
     if (tid < 64) ((uint32_t *)(smem + kZ))[tid] = 0u;

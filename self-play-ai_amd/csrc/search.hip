@@ -77,6 +77,9 @@ __device__ __forceinline__ void backup(uint4 *nodes, const uint32_t *path, int d
 __global__ __launch_bounds__(kBlock) void k_select(TreeView T, BatchView B, const uint32_t *__restrict__ active,
                                                    uint32_t n_active, float c, uint32_t *err) {
     const uint32_t gi = (blockIdx.x * blockDim.x + threadIdx.x) / kLanesPerTree;
+#ifdef SPAI_TREE_PRIO
+    __builtin_amdgcn_s_setprio(SPAI_TREE_PRIO);   // experiment: issue priority against the co-resident forward
+#endif
     const int lane8 = threadIdx.x & (kLanesPerTree - 1);
     if (gi >= n_active) return;
     const uint32_t t = active[gi];
