@@ -104,6 +104,9 @@ __device__ __forceinline__ int row_chunk(int v, int c) { return v * kStride + (c
 #ifndef SPAI_CHESS_PIN
 #define SPAI_CHESS_PIN 1
 #endif
+#ifndef SPAI_CHESS_TAP_UNROLL
+#define SPAI_CHESS_TAP_UNROLL 9   // taps per iteration of the tap loop (9: fully unrolled, 1.92 vs 1.99 ms)
+#endif
 template <int TAPS, int CB, int NT>
 __device__ __forceinline__ void conv(const uint8_t *smem, int in, const uint4 *__restrict__ w,
                                      const float *__restrict__ bias, int wave, int lane, f32x4 (&acc)[kCPW][NT]) {
@@ -153,6 +156,7 @@ __device__ __forceinline__ void conv(const uint8_t *smem, int in, const uint4 *_
         // taps as a runtime loop, channel blocks unrolled: ring slots stay static
 #pragma unroll
         for (int k = 0; k < DB - 1; ++k) load_b(k, B[k]);
+#pragma unroll SPAI_CHESS_TAP_UNROLL
         for (int tap = 0; tap < TAPS; ++tap) {
 #pragma unroll
             for (int cb = 0; cb < CB; ++cb) {
