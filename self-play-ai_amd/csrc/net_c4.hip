@@ -538,6 +538,9 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
     make_geo<W, 4, NPT>(lane, g);
     __syncthreads();
     stamp(P, W, lane, 1);
+#ifdef SPAI_C4_BLOCK_UNROLL
+#pragma unroll SPAI_C4_BLOCK_UNROLL
+#endif
     for (int b = 0; b < P.blocks; ++b) {   // relu(x + BN(conv(relu(BN(conv(x)))))), model/mod.rs:152-165
         f32x4 acc[Plan<W, 4, NPT>::n];
         const int l1 = 2 * b, l2 = 2 * b + 1;
