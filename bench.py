@@ -9,17 +9,19 @@ iteration).  value = MCTS simulations per second summed over all ranks.
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): games are
 sharded by id across ranks (rank r plays ids [r*G, (r+1)*G) per step), no
-collective touches the data path; gloo carries only the timing barrier and the
-max/sum reductions.  The GPU process never imports torch at N=1 (torch ships
-its own HIP runtime).
+collective touches the data path; a rank-0 TCP star (hostgroup.py, not torch
+gloo) carries only the timing barrier and the max/sum reductions.  The GPU
+process never imports torch (torch ships its own HIP runtime with the same
+SONAME).
 
 Adds to the JSON line:
   roofline      the fused forward kernel (dominant): algorithmic FLOPs of the
                 evaluated leaves / HIP-event time of the sampled launches
                 (engine stream), vs the 2.5 PF dense bf16 MFMA peak
-  cpu_baseline  the CPU restatement (oracle/: reference data layout, AoS
-                arena with State clones, sequential tree loop) with the net on
-                libtorch CPU fp32, run in a subprocess for a bounded window
+  cpu_baseline  the CPU restatement (oracle/refcpu.py: reference data layout,
+                AoS arena with State clones, sequential tree loop) with the net
+                on libtorch CPU fp32, run in a subprocess for a bounded window;
+                games/s from the committed completed-games record
 """
 import argparse
 import json
@@ -72,118 +74,44 @@ def parse():
 
 
 # ---------------------------------------------------------------- CPU baseline (subprocess)
-def cpu_baseline(args):
-    """Oracle self-play (reference algorithm and data layout) + libtorch CPU fp32
-    forward, for a bounded wall-time window; prints one JSON line."""
-    import ctypes as C
-
-    import numpy as np
-    import torch
-    import torch.nn.functional as F
-
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import oracle as O
-
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    L = O.lib()
-    p = torch.from_numpy(O.init_params(O.GAME_CONNECT4, args.blocks, 64, args.seed))
-    off = [0]
-
-    def take(*shape):
-        n = int(np.prod(shape))
-        v = p[off[0]:off[0] + n].reshape(shape)
-        off[0] += n
-        return v
-
-    def cbn(ci, co):
-        return [take(co, ci, 3, 3), take(co), take(co), take(co), take(co), take(co)]
-
-    stem = cbn(3, 64)
-    blocks = [(cbn(64, 64), cbn(64, 64)) for _ in range(args.blocks)]
-    pol = cbn(64, 32)
-    pw, pb = take(7, 1344), take(7)
-    val = cbn(64, 3)
-    vw, vb = take(1, 126), take(1)
-
-    def conv_bn(t, c, relu):
-        w, b, g, be, mu, var = c
-        t = F.batch_norm(F.conv2d(t, w, b, padding=1), mu, var, g, be, training=False, eps=1e-5)
-        return F.relu(t) if relu else t
-
-    enc = np.zeros((args.cpu_games, 126), np.float32)
-    deadline = [None]
-    iters = [0]
-
-    class Stop(Exception):
-        pass
-
-    def evaluate(user, n, states, priors, values):
-        # Model::predict on the CPU (model/mod.rs:36-98): encode, forward, softmax, mask
-        L.or_encode_states(O.GAME_CONNECT4, n, states, enc.ctypes.data_as(C.POINTER(C.c_float)))
-        with torch.no_grad():
-            t = torch.from_numpy(enc[:n]).view(-1, 3, 6, 7)
-            t = conv_bn(t, stem, True)
-            for c1, c2 in blocks:
-                t = F.relu(t + conv_bn(conv_bn(t, c1, True), c2, False))
-            lg = F.linear(conv_bn(t, pol, True).flatten(1), pw, pb)
-            v = torch.tanh(F.linear(conv_bn(t, val, True).flatten(1), vw, vb)).view(-1)
-            sm = torch.softmax(lg, -1).numpy()
-        legal = enc[:n].reshape(n, 3, 6, 7)[:, 2, 5, :]
-        m = sm * legal
-        m /= m.sum(1, keepdims=True)
-        pr = np.ctypeslib.as_array(priors, (n, 7))
-        pr[:] = m
-        np.ctypeslib.as_array(values, (n,))[:] = v.numpy()
-        iters[0] += 1
-
-    # run whole moves until the window closes; count simulations of completed moves
-    trees = [L.or_tree_create(O.GAME_CONNECT4) for _ in range(args.cpu_games)]
-    arr = (C.c_void_p * len(trees))(*trees)
-    n = len(trees)
-    pol_o = np.zeros((n, 7), np.float32)
-    ids = np.zeros((n, 7), np.int32)
-    vis = np.zeros((n, 7), np.float32)
-    nc = np.zeros(n, np.int32)
-    cb = O.EVAL_FN(evaluate)
-    t0 = time.perf_counter()
-    sims = 0
-    moves = 0
-    chunk = 50   # search iterations per call; the reference runs 800 per move
-    while time.perf_counter() - t0 < args.cpu_seconds and moves < 4:
-        done = 0
-        while done < args.sims and time.perf_counter() - t0 < args.cpu_seconds:
-            k = min(chunk, args.sims - done)
-            L.or_search(arr, n, k, 2.0, O.EVAL_NET, None, cb, None, O._f(pol_o), O._i(ids), O._f(vis), O._i(nc))
-            done += k
-            sims += n * k
-        if done < args.sims:
-            break
-        moves += 1
-        for i, t in enumerate(trees):   # advance on the most visited child, as a move would
-            j = int(np.argmax(vis[i, :nc[i]]))
-            L.or_tree_use_subtree(t, int(ids[i, j]))
-    dt = time.perf_counter() - t0
-    for t in trees:
-        L.or_tree_destroy(t)
-    sps = sims / dt
-    print(json.dumps({"value": sps, "unit": "sims/s", "cores": threads, "kind": "port",
-                      "sample": f"{args.cpu_games} C4 games from the empty board, {sims // n} search iterations "
-                                f"(800 sims/move) in {dt:.1f}s: oracle tree loop (AoS arena, State clones, "
-                                f"sequential) + libtorch CPU fp32 {args.blocks}x64 forward on {threads} threads; "
-                                f"games/s estimate = sims/s / (800 x plies per game)",
-                      "cpu_model": _cpu_model()}))
+CPU_RECORD = os.path.join(REPO, "profiles", "r02", "cpu_baseline.json")
 
 
-def _cpu_model():
+def cpu_record():
+    """the committed CPU record (scripts/cpu_games_baseline.py on the GPU box's host):
+    the thread sweep and a run of whole games to completion at 800 sims/move"""
     try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return "unknown"
+        with open(CPU_RECORD) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(args):
+    """Oracle tree loop (reference algorithm and data layout) + libtorch CPU fp32
+    forward (oracle/refcpu.py) for a bounded window; prints one JSON line."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import refcpu
+
+    rec = cpu_record()
+    threads = args.cpu_threads or (rec or {}).get("best_threads") or refcpu.cpu_quota()
+    r = refcpu.sims_window(args.cpu_games, args.sims, args.cpu_seconds, blocks=args.blocks, seed=args.seed,
+                           threads=threads)
+    out = {"value": r["sims_per_sec"], "unit": "sims/s", "cores": threads, "kind": "port",
+           "sample": f"{args.cpu_games} C4 games from the empty board, {r['sims_done'] // args.cpu_games} search "
+                     f"iterations ({args.sims} sims/move, {r['moves_completed']} whole moves) in {r['seconds']:.1f}s: "
+                     f"oracle tree loop (AoS arena, State clones, sequential) + libtorch CPU fp32 {args.blocks}x64 "
+                     f"forward on {threads} threads (thread count = best of the committed sweep)",
+           "cpu_model": refcpu.cpu_model(), "os_cpu_count": os.cpu_count(), "cpu_quota": refcpu.cpu_quota()}
+    if rec and "games_run" in rec:
+        g = rec["games_run"]
+        out["games_per_sec"] = g["games_per_sec"]
+        out["games_sample"] = (f"{g['games']} games played to completion at {args.sims} sims/move "
+                               f"({g['positions']} positions, mean {g['mean_plies']:.1f} plies, {g['seconds']:.0f}s) "
+                               f"on {g['threads']} threads; record {os.path.relpath(CPU_RECORD, REPO)} "
+                               f"({rec.get('cpu_model', '?')}, cpu quota {rec.get('cpu_quota', '?')})")
+        out["games_sims_per_sec"] = g["sims_per_sec"]
+    print(json.dumps(out))
 
 
 def run_cpu_baseline(args):
@@ -321,6 +249,13 @@ def main():
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         cb = run_cpu_baseline(args)
         result["cpu_baseline"] = cb
+        # BASELINE.md publishes no number for this metric: the ratio is against the
+        # CPU reference path measured on this box's host cores (same unit)
+        if cb.get("value"):
+            result["vs_baseline"] = result["value"] / cb["value"]
+            result["vs_baseline_basis"] = "sims/s over cpu_baseline.value (CPU reference path, this host)"
+        if cb.get("games_per_sec"):
+            result["vs_cpu_games_per_sec"] = result["games_per_sec"] / cb["games_per_sec"]
     if dist.rank == 0:
         print(json.dumps(result), flush=True)
     dist.close()

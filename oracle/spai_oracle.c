@@ -349,9 +349,12 @@ int or_weighted_index(const float *visits, int n, float temperature, double u) {
     }
     if (!(total > 0.0)) return -2;  /* WeightedIndex::new(..).unwrap() panics */
     double x = u * total;
-    for (int i = 0; i < n; ++i)
+    int last = 0;  /* WeightedIndex never returns a zero-weight item: fall back to the last nonzero one */
+    for (int i = 0; i < n; ++i) {
         if (cum[i] > x) return i;
-    return n - 1;
+        if (i == 0 ? cum[0] > 0.0 : cum[i] > cum[i - 1]) last = i;
+    }
+    return last;
 }
 
 /* Policy::get_best_action (connect_four.rs:116-124): Iterator::max_by with

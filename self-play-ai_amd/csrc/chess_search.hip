@@ -94,7 +94,6 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void k_cleaf(TV T, BV B, const
     uint32_t node = T.root[t];
     int d = 0;
     if (lane == 0) path[0] = node;
-    bool nan = false;
     for (;;) {
         const uint4 rec = T.nodes[base + node];
         const uint32_t nch = rec.w >> 16;
@@ -103,6 +102,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void k_cleaf(TV T, BV B, const
         const float sq = sqrtf((float)rec.x);
         float bu = -INFINITY;
         int bi = -1;
+        bool nan = false;
         for (uint32_t i = lane; i < nch; i += 64) {
             const float u = ucb(sq, T.nodes[base + f + i], c);
             nan |= u != u;
@@ -110,6 +110,12 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void k_cleaf(TV T, BV B, const
                 bu = u;
                 bi = (int)i;
             }
+        }
+        // a NaN on any child panics in the reference (mcts.rs:106-109): stop the
+        // whole wave before the argmax so its lanes never walk different children
+        if (__ballot(nan)) {
+            if (lane == 0) atomicOr(err, kErrNan);
+            return;
         }
 #pragma unroll
         for (int m = 1; m < 64; m <<= 1) {
@@ -129,7 +135,6 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void k_cleaf(TV T, BV B, const
         }
         if (lane == 0) path[d] = node;
     }
-    if (nan && lane == 0) atomicOr(err, kErrNan);
     __builtin_amdgcn_wave_barrier();
     // the leaf: legal moves, repetition count, status (chess.rs:51-61,150-174)
     const GenOut g = wave_movegen(b, T.leaf_moves + (size_t)t * kMaxMoves, lane);

@@ -48,9 +48,12 @@ inline int weighted_index(const float *visits, int n, float temperature, double 
     }
     if (!(total > 0.0)) return -2;
     double x = u * total;
-    for (int i = 0; i < n; ++i)
+    int last = 0;   // last index whose cumulative weight increased (rand never picks a zero weight)
+    for (int i = 0; i < n; ++i) {
         if (cum[i] > x) return i;
-    return n - 1;
+        if (i == 0 ? cum[0] > 0.0 : cum[i] > cum[i - 1]) last = i;
+    }
+    return last;   // u * total rounded up to total
 }
 
 }  // namespace spai

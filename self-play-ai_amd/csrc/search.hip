@@ -93,7 +93,6 @@ __global__ __launch_bounds__(kBlock) void k_select(TreeView T, BatchView B, cons
     uint32_t p0 = node, p1 = 0, p2 = 0, p3 = 0, p4 = 0, p5 = 0;
     int d = 0;
     if (lane8 == 0) path[0] = node;
-    bool nan = false;
     while (rec.w != kNoChildren) {                          // while node.is_fully_expanded()
         const uint32_t first = rec.w & 0xFFFFFFu, nch = rec.w >> 24;
         uint4 ch = make_uint4(0, 0, 0, 0);
@@ -101,7 +100,13 @@ __global__ __launch_bounds__(kBlock) void k_select(TreeView T, BatchView B, cons
         if ((uint32_t)lane8 < nch) {
             ch = nodes[first + lane8];
             u = ucb(rec.x, ch, c);
-            nan |= u != u;
+        }
+        // a NaN on ANY child panics in the reference (partial_cmp().unwrap(),
+        // mcts.rs:106-109): OR over the tree's 8 lanes and stop the whole group
+        // before the argmax, so lanes never split onto different children
+        if ((__ballot(u != u) >> (threadIdx.x & 63 & ~(kLanesPerTree - 1))) & 0xFFull) {
+            if (lane8 == 0) atomicOr(err, kErrNan);
+            return;
         }
         // argmax with ties to the LAST child (Iterator::max_by, mcts.rs:110-113)
         float bu = u;
@@ -145,7 +150,6 @@ __global__ __launch_bounds__(kBlock) void k_select(TreeView T, BatchView B, cons
             }
         }
     }
-    if (nan && lane8 == 0) atomicOr(err, kErrNan);
     if (lane8 == 0) T.depth[t] = (uint8_t)d;
     if (status != c4::kOngoing) {                           // terminal leaf: backprop(leaf, value), mcts.rs:245-247
         const float v = c4::terminal_value(status);

@@ -270,7 +270,6 @@ __global__ __launch_bounds__(64) void k_tleaf(TV T, BV B, const uint32_t *__rest
     uint32_t node = T.root[t];
     int d = 0;
     if (lane == 0) path[0] = node;
-    bool nan = false;
     uint4 rec = nodes[node];
     while (rec.w != kNoChildren) {
         const uint32_t first = rec.w & 0xFFFFFFu, nch = rec.w >> 24;
@@ -280,7 +279,11 @@ __global__ __launch_bounds__(64) void k_tleaf(TV T, BV B, const uint32_t *__rest
         if ((uint32_t)lane < nch) {
             ch = nodes[first + lane];
             u = ucb(sq, ch, c);
-            nan |= u != u;
+        }
+        // NaN on any child: the reference panics (mcts.rs:106-109); stop before the argmax
+        if (__ballot(u != u)) {
+            if (lane == 0) atomicOr(err, kErrNan);
+            return;
         }
         float bu = u;
         int bi = (uint32_t)lane < nch ? lane : -1;
@@ -303,7 +306,6 @@ __global__ __launch_bounds__(64) void k_tleaf(TV T, BV B, const uint32_t *__rest
         ++d;
         if (lane == 0) path[d] = node;
     }
-    if (nan && lane == 0) atomicOr(err, kErrNan);
     __syncthreads();
     if (s.status != SPAI_ONGOING) {   // terminal: Won -> -1, Tied -> 0 (tictactoe.rs:188-197)
         backup(nodes, path, d, s.status == SPAI_WON ? -1.0f : 0.0f, lane);

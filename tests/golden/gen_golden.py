@@ -263,10 +263,13 @@ def weighted_index(visits, temperature, u):
         total += math.pow(float(v), float(f32(temperature)))
         cum.append(total)
     x = u * total
+    last = 0   # never a zero-weight item (rand's WeightedIndex)
     for i, cv in enumerate(cum):
         if cv > x:
             return i
-    return len(cum) - 1
+        if cv > (cum[i - 1] if i else 0.0):
+            last = i
+    return last
 
 
 def splitmix64(x):
