@@ -10,6 +10,9 @@ O=gpurun_out/$TAG
 mkdir -p $O
 STEPS=${STEPS:-"tests bench trace prof prof1 cpusweep"}
 { nproc; cat /sys/fs/cgroup/cpu.max 2>/dev/null; grep -m1 "model name" /proc/cpuinfo; } > $O/host.txt
+( while true; do sleep 50; date +%s >> $O/heartbeat; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
 has() { case " $STEPS " in *" $1 "*) return 0;; esac; return 1; }
 stats() {   # $1 = name, rest = env for the profiled bench
   local n=$1; shift
@@ -38,6 +41,10 @@ if has trace; then
 fi
 if has prof; then stats two SPAI_UNUSED=0 || exit $?; fi
 if has prof1; then stats one SPAI_CHAINS=1 || exit $?; fi
+if has ubench; then
+  timeout -k 10 120 ./scripts/ubench/weight_stream > $O/ubench_weight_stream.txt 2>&1
+  rc=$?; cat $O/ubench_weight_stream.txt; echo "ubench rc=$rc"; [ $rc -eq 0 ] || exit $rc
+fi
 if has cpusweep; then
   timeout -k 10 900 python scripts/cpu_games_baseline.py --out $O/cpu_sweep.json --no-games > $O/cpu_sweep.log 2>&1
   rc=$?; tail -2 $O/cpu_sweep.log; echo "cpu sweep rc=$rc"; [ $rc -eq 0 ] || exit $rc
