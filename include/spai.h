@@ -56,6 +56,12 @@ typedef enum spai_status { SPAI_ONGOING = 0, SPAI_TIED = 1, SPAI_WON = 2 } spai_
  * search and self-play bit-exactly against the CPU oracle. */
 typedef enum spai_eval { SPAI_EVAL_NET = 0, SPAI_EVAL_UNIFORM = 1, SPAI_EVAL_HASH = 2 } spai_eval;
 
+/* Arithmetic of a device net.  BF16: bf16 weights and activations on the MFMA
+ * matrix cores, fp32 accumulate (the throughput path).  F32: the reference's
+ * own fp32 arithmetic (model/mod.rs:36-98 runs libtorch in fp32), each output
+ * summed in the CPU oracle's order, for parity work. */
+typedef enum spai_dtype { SPAI_DTYPE_BF16 = 0, SPAI_DTYPE_F32 = 1 } spai_dtype;
+
 typedef struct spai_c4_state {
     uint64_t x;                  /* X stones, bit col*7+row */
     uint64_t o;                  /* O stones */
@@ -119,7 +125,8 @@ int spai_rules_bench(spai_engine *eng, uint32_t n, uint32_t iters, double *ms);
  * registers them for model/connect_four.rs:34-44.  Device path: hidden = 64. */
 int spai_net_num_params(int game, int blocks, int hidden, size_t *count);
 int spai_net_init_params(int game, int blocks, int hidden, uint64_t seed, float *params);
-int spai_net_create(spai_engine *eng, int blocks, int hidden, const float *params, size_t nparams,
+/* Net::new (model/mod.rs:22-28) with its weights: dtype = spai_dtype */
+int spai_net_create(spai_engine *eng, int blocks, int hidden, const float *params, size_t nparams, int dtype,
                     spai_net **out);
 int spai_net_destroy(spai_net *net);
 /* Net::forward(x, train=false): x [n][3][6][7] f32 -> logits [n][7], value [n] (tanh) */

@@ -273,10 +273,11 @@ int spai_net_init_params(int game, int blocks, int hidden, uint64_t seed, float 
     return SPAI_OK;
 }
 
-int spai_net_create(spai_engine *e, int blocks, int hidden, const float *params, size_t nparams, spai_net **out) {
+int spai_net_create(spai_engine *e, int blocks, int hidden, const float *params, size_t nparams, int dtype,
+                    spai_net **out) {
     ENG_CHECK(e);
     PTR_CHECK(out);
-    return net_create(e, blocks, hidden, params, nparams, out);
+    return net_create(e, blocks, hidden, params, nparams, dtype, out);
 }
 
 int spai_net_destroy(spai_net *n) {

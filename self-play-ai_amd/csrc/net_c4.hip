@@ -766,13 +766,29 @@ size_t net_num_params(int game, int blocks, int hidden) {
     return n;
 }
 
-int net_create(spai_engine *e, int blocks, int hidden, const float *params, size_t nparams, spai_net **out) {
+int net_create(spai_engine *e, int blocks, int hidden, const float *params, size_t nparams, int dtype,
+               spai_net **out) {
     SPAI_CHECK(e->game == SPAI_GAME_CONNECT4, SPAI_ERR_UNSUPPORTED, "device net: only Connect4 is built");
+    SPAI_CHECK(dtype == SPAI_DTYPE_BF16 || dtype == SPAI_DTYPE_F32, SPAI_ERR_INVALID, "unknown dtype %d", dtype);
     SPAI_CHECK(hidden == kHid, SPAI_ERR_UNSUPPORTED, "device net: hidden must be 64 (got %d)", hidden);
     SPAI_CHECK(blocks >= 0 && blocks <= kMaxBlocks, SPAI_ERR_UNSUPPORTED, "device net: 0..%d blocks (got %d)",
                kMaxBlocks, blocks);
     SPAI_CHECK(params && nparams == net_num_params(e->game, blocks, hidden), SPAI_ERR_INVALID,
                "expected %zu params, got %zu", net_num_params(e->game, blocks, hidden), nparams);
+    if (dtype == SPAI_DTYPE_F32) {   // the reference's fp32 arithmetic (net_c4_f32.hip)
+        spai_net *n = new spai_net();
+        n->eng = e;
+        n->blocks = blocks;
+        n->hidden = hidden;
+        n->dtype = SPAI_DTYPE_F32;
+        const int rc = net_create_f32(n, params);
+        if (rc != SPAI_OK) {
+            net_destroy(n);
+            return rc;
+        }
+        *out = n;
+        return SPAI_OK;
+    }
     // walk the parameter list in construction order
     const float *p = params;
     auto take_conv = [&](int ci, int co) {
@@ -892,7 +908,7 @@ int net_create(spai_engine *e, int blocks, int hidden, const float *params, size
 void net_destroy(spai_net *n) {
     if (!n) return;
     for (auto *b : {&n->w_stem, &n->w_res, &n->w_head, &n->w_lin}) b->release();
-    for (auto *b : {&n->b_stem, &n->b_res, &n->b_head, &n->b_pol, &n->b_val, &n->io_x,
+    for (auto *b : {&n->b_stem, &n->b_res, &n->b_head, &n->b_pol, &n->b_val, &n->f32, &n->io_x,
                     &n->io_logits, &n->io_value, &n->io_priors})
         b->release();
     n->io_mine.release();
@@ -935,6 +951,7 @@ int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
     SPAI_CHECK(false, SPAI_ERR_UNSUPPORTED, "phase stamps need the diagnostic build (make -C self-play-ai_amd diag)");
 #endif
     SPAI_CHECK(cnt > 0, SPAI_ERR_INVALID, "need cnt > 0");
+    SPAI_CHECK(n->dtype == SPAI_DTYPE_BF16, SPAI_ERR_UNSUPPORTED, "phase stamps time the bf16 kernel");
     SPAI_TRY(ensure_io(n, cnt));
     hipStream_t st = n->eng->stream;
     std::vector<uint64_t> m(cnt), t(cnt);
@@ -988,6 +1005,7 @@ int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
 int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint32_t max_n, const uint64_t *mine,
                    const uint64_t *theirs, float *priors, float *value) {
     if (!max_n) return SPAI_OK;
+    if (net->dtype == SPAI_DTYPE_F32) return net_f32_launch(net, st, d_count, max_n, mine, theirs, nullptr, priors, value, nullptr);
     // SPAI_FWD_GRID caps the persistent grid (tuning knob: fewer workgroups -> larger groups S)
     static const uint32_t grid_cap = [] {
         const char *v = std::getenv("SPAI_FWD_GRID");
@@ -1007,9 +1025,13 @@ int net_forward_x(spai_net *n, uint32_t cnt, const float *x, float *logits, floa
     SPAI_TRY(ensure_io(n, cnt));
     hipStream_t st = n->eng->stream;
     SPAI_HIP(hipMemcpyAsync(n->io_x.p, x, (size_t)cnt * 126 * 4, hipMemcpyHostToDevice, st));
-    k_forward<true><<<(cnt + kS - 1) / kS, kThreads, 0, st>>>(nullptr, cnt, kS, nullptr, nullptr, n->io_x.p,
-                                                             params_of(n), nullptr, n->io_value.p, n->io_logits.p);
-    SPAI_HIP(hipGetLastError());
+    if (n->dtype == SPAI_DTYPE_F32) {
+        SPAI_TRY(net_f32_launch(n, st, nullptr, cnt, nullptr, nullptr, n->io_x.p, nullptr, n->io_value.p, n->io_logits.p));
+    } else {
+        k_forward<true><<<(cnt + kS - 1) / kS, kThreads, 0, st>>>(nullptr, cnt, kS, nullptr, nullptr, n->io_x.p,
+                                                                 params_of(n), nullptr, n->io_value.p, n->io_logits.p);
+        SPAI_HIP(hipGetLastError());
+    }
     SPAI_HIP(hipMemcpyAsync(logits, n->io_logits.p, (size_t)cnt * 28, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipMemcpyAsync(value, n->io_value.p, (size_t)cnt * 4, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipStreamSynchronize(st));
@@ -1028,9 +1050,15 @@ int net_predict(spai_net *n, uint32_t cnt, const spai_c4_state *states, float *p
     hipStream_t st = n->eng->stream;
     SPAI_HIP(hipMemcpyAsync(n->io_mine.p, m.data(), (size_t)cnt * 8, hipMemcpyHostToDevice, st));
     SPAI_HIP(hipMemcpyAsync(n->io_theirs.p, t.data(), (size_t)cnt * 8, hipMemcpyHostToDevice, st));
-    k_forward<false><<<std::min<uint32_t>(cnt, (uint32_t)n->n_cu), kThreads, 0, st>>>(
-        nullptr, cnt, 0, n->io_mine.p, n->io_theirs.p, nullptr, params_of(n), n->io_priors.p, n->io_value.p, nullptr);
-    SPAI_HIP(hipGetLastError());
+    if (n->dtype == SPAI_DTYPE_F32) {
+        SPAI_TRY(net_f32_launch(n, st, nullptr, cnt, n->io_mine.p, n->io_theirs.p, nullptr, n->io_priors.p,
+                                n->io_value.p, nullptr));
+    } else {
+        k_forward<false><<<std::min<uint32_t>(cnt, (uint32_t)n->n_cu), kThreads, 0, st>>>(
+            nullptr, cnt, 0, n->io_mine.p, n->io_theirs.p, nullptr, params_of(n), n->io_priors.p, n->io_value.p,
+            nullptr);
+        SPAI_HIP(hipGetLastError());
+    }
     std::vector<float> pr((size_t)cnt * kPriorStride);
     SPAI_HIP(hipMemcpyAsync(pr.data(), n->io_priors.p, pr.size() * 4, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipMemcpyAsync(values, n->io_value.p, (size_t)cnt * 4, hipMemcpyDeviceToHost, st));

@@ -192,7 +192,7 @@ int pipeline_run(const spai_pipeline_config *cfg, const float *init_params, size
             if (ver != have) {   // refresh the self-play net from the published weights
                 if (net) spai_net_destroy(net);
                 net = nullptr;
-                rc = spai_net_create(e, cfg->blocks, 64, params.data(), params.size(), &net);
+                rc = spai_net_create(e, cfg->blocks, 64, params.data(), params.size(), SPAI_DTYPE_BF16, &net);
                 if (rc == SPAI_OK) rc = spai_engine_set_net(e, net);
                 have = ver;
             }

@@ -121,6 +121,8 @@ struct spai_net {
     // packed, BN-folded bf16 MFMA fragments + fp32 biases / head linears (see net_c4.hip)
     spai::DevBuf<uint16_t> w_stem, w_res, w_head, w_lin;
     spai::DevBuf<float> b_stem, b_res, b_head, b_pol, b_val;
+    int dtype = SPAI_DTYPE_BF16;    // SPAI_DTYPE_F32: unfolded fp32 weights in `f32` (net_c4_f32.hip)
+    spai::DevBuf<float> f32;
     spai::DevBuf<float> io_x, io_logits, io_value, io_priors;   // scratch for forward/predict calls
     spai::DevBuf<uint64_t> io_mine, io_theirs;
     spai::DevBuf<uint32_t> io_count;
@@ -190,7 +192,8 @@ int rules_mask(spai_engine *e, uint32_t first, uint32_t n, const float *p, uint3
 int rules_bench(spai_engine *e, uint32_t n, uint32_t iters, double *ms);
 
 // net_c4.hip
-int net_create(spai_engine *e, int blocks, int hidden, const float *params, size_t nparams, spai_net **out);
+int net_create(spai_engine *e, int blocks, int hidden, const float *params, size_t nparams, int dtype,
+               spai_net **out);
 void net_destroy(spai_net *net);
 int net_forward_x(spai_net *net, uint32_t n, const float *x, float *logits, float *value);
 int net_predict(spai_net *net, uint32_t n, const spai_c4_state *states, float *priors, float *values);
@@ -200,6 +203,11 @@ void net_init_params(int game, int blocks, int hidden, uint64_t seed, float *par
 // evaluate `count` (device scalar) leaves of the batch; grid sized for max_n
 int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint32_t max_n,
                    const uint64_t *mine, const uint64_t *theirs, float *priors, float *value);
+
+// net_c4_f32.hip
+int net_create_f32(spai_net *n, const float *params);
+int net_f32_launch(spai_net *n, hipStream_t st, const uint32_t *d_count, uint32_t max_n, const uint64_t *mine,
+                   const uint64_t *theirs, const float *x, float *priors, float *value, float *logits);
 
 // learner.hip
 int learner_create(spai_engine *e, int blocks, int hidden, const float *params, size_t n, const spai_adam_config *cfg,

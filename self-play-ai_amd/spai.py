@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("SPAI_LIB") or os.path.join(HERE, "libspai.so")
 
 GAME_TICTACTOE, GAME_CONNECT4, GAME_CHESS = 0, 1, 2
 EVAL_NET, EVAL_UNIFORM, EVAL_HASH = 0, 1, 2
+DTYPE_BF16, DTYPE_F32 = 0, 1   # spai_dtype
 ONGOING, TIED, WON = 0, 1, 2
 OK = 0
 ERRORS = {-1: "INVALID", -2: "ILLEGAL_MOVE", -3: "GAME_OVER", -4: "DEVICE", -5: "NAN", -6: "CAPACITY",
@@ -133,7 +134,7 @@ def lib():
         L.spai_rules_bench.argtypes = [vp, u32, u32, vp]
         L.spai_net_num_params.argtypes = [i32, i32, i32, P(C.c_size_t)]
         L.spai_net_init_params.argtypes = [i32, i32, i32, u64, vp]
-        L.spai_net_create.argtypes = [vp, i32, i32, vp, C.c_size_t, P(vp)]
+        L.spai_net_create.argtypes = [vp, i32, i32, vp, C.c_size_t, i32, P(vp)]
         L.spai_net_destroy.argtypes = [vp]
         L.spai_net_forward.argtypes = [vp, u32, vp, vp, vp]
         L.spai_predict.argtypes = [vp, u32, vp, vp, vp]
@@ -216,11 +217,12 @@ def states_array(states):
 class Net:
     """Net (model/mod.rs:22-28) on the device; Model::predict as .predict()."""
 
-    def __init__(self, engine, blocks, params, hidden=64):
+    def __init__(self, engine, blocks, params, hidden=64, dtype=None):
         params = np.ascontiguousarray(params, np.float32)
         self.engine, self.blocks, self.hidden = engine, blocks, hidden
+        self.dtype = DTYPE_BF16 if dtype is None else dtype
         h = C.c_void_p()
-        _check(lib().spai_net_create(engine.h, blocks, hidden, _p(params), params.size, C.byref(h)))
+        _check(lib().spai_net_create(engine.h, blocks, hidden, _p(params), params.size, self.dtype, C.byref(h)))
         self.h = h
 
     def close(self):

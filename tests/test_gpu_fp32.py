@@ -1,0 +1,171 @@
+"""The fp32 Connect4 net (spai_net_create with SPAI_DTYPE_F32) against the CPU
+oracle: the reference's own arithmetic (model/mod.rs:36-98 runs libtorch in
+fp32), so search and self-play driven by the real net are checked to the bit.
+
+Tolerances: conv and linear outputs are summed in the oracle's order with
+separate multiply and add, so logits are compared bit-exactly; tanh / exp come
+from the device libm, not glibc, so values and priors may differ in the last
+ulp (2e-7 absolute).  Search visit counts and the self-play sample stream are
+compared exactly against tests/golden/mcts_f32net.npz (gen_f32net_golden.py).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+ULP_TOL = dict(rtol=0, atol=2e-7)
+
+
+@pytest.fixture(scope="module")
+def spai():
+    import spai as s
+    s.lib()
+    return s
+
+
+def _positions(oracle, n, seed):
+    rng = np.random.default_rng(seed)
+    acts = rng.integers(0, 7, size=(n, 30)).astype(np.int32)
+    ref = oracle.c4_replay(acts)
+    out = []
+    for g in range(n):
+        ply = int(rng.integers(0, 30))
+        while ply > 0 and ref["status"][g, ply] != 0:
+            ply -= 1
+        out.append((int(ref["x"][g, ply]), int(ref["o"][g, ply]), ply))
+    return out
+
+
+def _encode(oracle, pos):
+    from test_gpu_parity import _oracle_state
+    return np.stack([_oracle_state(oracle, x, o, n, 0).encoding().ravel() for x, o, n in pos])
+
+
+@pytest.mark.parametrize("blocks", [0, 2, 6])
+def test_f32_forward_bit_exact_vs_oracle(spai, oracle, blocks):
+    p = spai.init_params(blocks, 64, seed=11)
+    e = spai.Engine(num_searches=1, max_trees=1)
+    net = spai.Net(e, blocks, p, dtype=spai.DTYPE_F32)
+    x = _encode(oracle, _positions(oracle, 40, seed=blocks))
+    x[-1] = np.random.default_rng(1).standard_normal(126).astype(np.float32)   # arbitrary input, not a board
+    lg, v = net.forward(x)
+    rl, rv = oracle.Net(oracle.GAME_CONNECT4, blocks, 64, p).forward(x)
+    np.testing.assert_array_equal(lg, rl)
+    np.testing.assert_allclose(v, rv, **ULP_TOL)
+    net.close()
+    e.close()
+
+
+def test_f32_forward_vs_libtorch_golden(spai):
+    """the fp32 mode against libtorch CPU fp32 at 1e-4"""
+    z = np.load(os.path.join(GOLDEN, "net_c4_2x64.npz"))
+    blocks = int(z["meta"][0])
+    e = spai.Engine(num_searches=1, max_trees=1)
+    net = spai.Net(e, blocks, z["params"], dtype=spai.DTYPE_F32)
+    lg, v = net.forward(z["x"])
+    np.testing.assert_allclose(lg, z["logits"], rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(v, z["value"], rtol=1e-4, atol=1e-4)
+    b = z["boards"]
+    pr, _ = net.predict([(int(b[i, 0]), int(b[i, 1]), int(b[i, 2]), 0) for i in range(len(b))])
+    np.testing.assert_allclose(pr, z["priors"], rtol=1e-4, atol=1e-5)
+    net.close()
+    e.close()
+
+
+def test_f32_predict_vs_oracle(spai, oracle):
+    """Model::predict: softmax then mask_invalid_actions (model/mod.rs:62-93)"""
+    from test_gpu_parity import _oracle_state
+    p = spai.init_params(2, 64, seed=4)
+    e = spai.Engine(num_searches=1, max_trees=1)
+    net = spai.Net(e, 2, p, dtype=spai.DTYPE_F32)
+    pos = _positions(oracle, 64, seed=8)
+    pr, pv = net.predict([(x, o, n, 0) for x, o, n in pos])
+    L = oracle.lib()
+    on = oracle.Net(oracle.GAME_CONNECT4, 2, 64, p)
+    sts = [_oracle_state(oracle, x, o, n, 0) for x, o, n in pos]
+    arr = (oracle.C.c_void_p * len(sts))(*[oracle.C.addressof(s.st) for s in sts])
+    rp = np.zeros((len(sts), 7), np.float32)
+    rv = np.zeros(len(sts), np.float32)
+    L.or_predict(on.h, len(sts), arr, oracle._f(rp), oracle._f(rv))
+    np.testing.assert_allclose(pr, rp, rtol=2e-6, atol=2e-7)
+    np.testing.assert_allclose(pv, rv, **ULP_TOL)
+    assert np.all((pr == 0) == (rp == 0))   # illegal columns exactly zero in both
+    net.close()
+    e.close()
+
+
+def _golden():
+    return np.load(os.path.join(GOLDEN, "mcts_f32net.npz"))
+
+
+def test_f32_net_search_matches_oracle(spai):
+    """Mcts::search with the fp32 net: root visit counts and policies of 48 trees
+    (two search chains) equal the oracle's"""
+    z = _golden()
+    roots, sims = z["roots"], int(z["sims"])
+    n = len(roots)
+    e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_NET, max_moves=2)
+    net = spai.Net(e, int(z["blocks"]), spai.init_params(int(z["blocks"]), 64, seed=int(z["seed"])),
+                   dtype=spai.DTYPE_F32)
+    e.set_net(net)
+    e.trees_create(n)
+    for i, (x, o, m) in enumerate(roots):
+        e.tree_reset(i, (int(x), int(o), int(m), 0))
+    pol, ids, vis, nc = e.search(np.arange(n), sims)
+    np.testing.assert_array_equal(nc, z["n_children"])
+    np.testing.assert_array_equal(vis, z["visits"])
+    np.testing.assert_array_equal(pol, z["policy"])
+    net.close()
+    e.close()
+
+
+def test_f32_net_self_play_matches_oracle(spai):
+    """SelfPlayWorker::self_play with the fp32 net: the whole sample stream
+    (encodings, visit policies, signed values, moves, emission order)"""
+    z = _golden()
+    n, sims, seed = int(z["sp_games"]), int(z["sp_sims"]), int(z["sp_seed"])
+    e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_NET, seed=seed)
+    net = spai.Net(e, int(z["blocks"]), spai.init_params(int(z["blocks"]), 64, seed=int(z["seed"])),
+                   dtype=spai.DTYPE_F32)
+    e.set_net(net)
+    games, stats = e.self_play(n)
+    k = 0
+    for g in games:
+        m = len(g["value"])
+        assert list(z["sp_game"][k:k + m]) == [g["game"]] * m
+        np.testing.assert_array_equal(g["policy"], z["sp_policy"][k:k + m])
+        np.testing.assert_array_equal(g["value"], z["sp_value"][k:k + m])
+        np.testing.assert_array_equal(g["enc"], z["sp_enc"][k:k + m])
+        assert list(g["moves"]) == list(z["sp_moves"][g["game"], :m])
+        k += m
+    assert k == len(z["sp_value"]) and stats["games"] == n
+    net.close()
+    e.close()
+
+
+def test_f32_and_bf16_nets_agree_on_search(spai):
+    """the bf16 throughput path against the fp32 path on the same roots: the root
+    visit distributions are close (bf16 moves priors by ~1e-2, so visits may
+    shift by a few, never the legal-move set)"""
+    z = _golden()
+    roots, sims = z["roots"], int(z["sims"])
+    n = len(roots)
+    p = spai.init_params(int(z["blocks"]), 64, seed=int(z["seed"]))
+    out = []
+    for dt in (spai.DTYPE_F32, spai.DTYPE_BF16):
+        e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_NET, max_moves=2)
+        net = spai.Net(e, int(z["blocks"]), p, dtype=dt)
+        e.set_net(net)
+        e.trees_create(n)
+        for i, (x, o, m) in enumerate(roots):
+            e.tree_reset(i, (int(x), int(o), int(m), 0))
+        out.append(e.search(np.arange(n), sims))
+        net.close()
+        e.close()
+    (pa, _, va, na), (pb, _, vb, nb) = out
+    np.testing.assert_array_equal(na, nb)
+    assert np.abs(pa - pb).max() < 0.25
+    assert np.mean(np.abs(pa - pb).sum(1)) < 0.15

@@ -247,3 +247,30 @@ def test_learner_oracle_vs_torch_golden(oracle):
     P1, _, _ = LR.train(p0, batches[:1], blocks, hidden)
     check_learner_params(P1, z["params1"], [g_ref], blocks, hidden, 1)
     check_learner_params(P3, z["params3"], [g_ref], blocks, hidden, 3, tol=1e-4)
+
+
+def test_mcts_f32net_fixture(oracle):
+    """tests/golden/mcts_f32net.npz (search with the fp32 net, gen_f32net_golden.py)
+    is reproducible by the oracle: the first 6 roots"""
+    z = np.load(os.path.join(GOLDEN, "mcts_f32net.npz"))
+    blocks, seed, sims = int(z["blocks"]), int(z["seed"]), int(z["sims"])
+    net = oracle.Net(oracle.GAME_CONNECT4, blocks, 64, oracle.init_params(oracle.GAME_CONNECT4, blocks, 64, seed))
+    L = oracle.lib()
+    roots = []
+    for x, o, n in z["roots"][:6]:
+        st = oracle.C4State()
+        L.or_c4_init(oracle.C.byref(st))
+        for col in range(7):
+            for row in range(6):
+                b = 1 << (col * 7 + row)
+                if int(x) & b:
+                    st.board[row][col] = oracle.X
+                elif int(o) & b:
+                    st.board[row][col] = oracle.O
+        st.num_actions_played = int(n)
+        st.current_player = oracle.X if int(n) % 2 == 0 else oracle.O
+        roots.append(oracle.C4(st))
+    rc, pol, ids, vis, nc = oracle.search_c4(roots, sims, eval_kind=oracle.EVAL_NET, net=net)
+    assert rc >= 0
+    np.testing.assert_array_equal(vis, z["visits"][:6])
+    np.testing.assert_array_equal(pol, z["policy"][:6])
