@@ -212,6 +212,10 @@ int spai_engine_timing_items(spai_engine *eng, double *total_ms, double *items);
  * epilogue end, barrier passed).  Needs the diagnostic build (SPAI_DIAG);
  * the production library returns SPAI_ERR_UNSUPPORTED.  Never on the timed path. */
 int spai_net_phase_cycles(spai_net *net, uint32_t count, double *cycles);
+/* Device time of the search's forward launch ALONE (nothing else on the GPU):
+ * ms = mean over `iters` back-to-back launches on `count` random reachable
+ * positions, HIP events on the engine stream.  Measurement only. */
+int spai_net_bench(spai_net *net, uint32_t count, uint32_t iters, double *ms);
 
 /* ---------------------------------------------------------------- learner
  * The training step of the C4 net on the device:
@@ -221,9 +225,12 @@ int spai_net_phase_cycles(spai_net *net, uint32_t count, double *cycles);
  * backward, and one Adam step (tch Adam::default(), lr 1e-3, model/mod.rs:107).
  * Parameters use spai_net_create's flat construction order, so
  * spai_learner_params() feeds spai_net_create() for the self-play replicas.
- * With a communicator (spai_learner_set_comm) the gradients are summed over
- * ranks with RCCL and scaled by 1/world, and the BN running statistics are
- * averaged: a data-parallel learner whose replicas stay identical. */
+ * With a communicator (spai_learner_set_comm) each rank's mean gradient is
+ * weighted by its share of the global batch (B_rank / sum B) and summed over
+ * ranks with RCCL, so a step equals one step on the union of the ranks'
+ * batches whatever their sizes; BatchNorm batch statistics stay per rank (DDP
+ * without SyncBN) and the running statistics are averaged, so the replicas
+ * stay identical. */
 typedef struct spai_learner spai_learner;
 typedef struct spai_adam_config {
     float lr;            /* 1e-3 */
@@ -257,6 +264,10 @@ int spai_learner_grads(spai_learner *l, float *grads, size_t n_params);
  * copy); world 1 with NULL drops the communicator. */
 int spai_comm_unique_id(uint8_t *id /* SPAI_COMM_ID_BYTES */);
 int spai_learner_set_comm(spai_learner *l, int rank, int world, const uint8_t *id);
+/* Weight refresh for self-play replicas (learner_concurrent.rs:158-159,260-264 hands the
+ * trainer's weights to the self-play workers): RCCL broadcast of rank `root`'s parameters
+ * to every rank of the communicator; a learner without one is left unchanged. */
+int spai_learner_broadcast(spai_learner *l, int root);
 
 /* ---------------------------------------------------------------- checkpoints
  * safetensors files with tch VarStore naming (VarStore::save / load,

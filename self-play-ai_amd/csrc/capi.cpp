@@ -376,6 +376,13 @@ int spai_net_phase_cycles(spai_net *n, uint32_t count, double *cycles) {
     return net_phase_stamps(n, count, cycles);
 }
 
+int spai_net_bench(spai_net *n, uint32_t count, uint32_t iters, double *ms) {
+    PTR_CHECK(n);
+    PTR_CHECK(ms);
+    ENG_CHECK(n->eng);
+    return net_bench(n, count, iters, ms);
+}
+
 int spai_engine_timing_items(spai_engine *e, double *total_ms, double *items) {
     ENG_CHECK(e);
     for (int i = 0; i < 3; ++i) {
@@ -447,6 +454,12 @@ int spai_learner_set_comm(spai_learner *l, int rank, int world, const uint8_t *i
     ENG_CHECK(l->eng);
     if (world > 1) PTR_CHECK(id);   // world 1: an id makes a 1-rank RCCL communicator, NULL none
     return learner_set_comm(l, rank, world, id);
+}
+
+int spai_learner_broadcast(spai_learner *l, int root) {
+    PTR_CHECK(l);
+    ENG_CHECK(l->eng);
+    return learner_broadcast(l, root);
 }
 
 // ---------------------------------------------------------------- checkpoints

@@ -513,6 +513,15 @@ __global__ void k_adam(float *__restrict__ p, const float *__restrict__ g, float
     p[i] -= (lr / bc1) * (mi / (sqrtf(vi) / bc2_sqrt + eps));
 }
 
+// data-parallel weighting: this rank's mean gradient times B_rank / sum over ranks of B
+__global__ void k_weight_grad(float *__restrict__ g, size_t n, float b_local, const float *__restrict__ b_sum) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    g[i] *= b_local / b_sum[0];
+}
+
+__global__ void k_set1(float *__restrict__ dst, float v) { *dst = v; }
+
 // running stats gathered into / scattered from a packed buffer (cross-rank average)
 __global__ void k_gather(const float *__restrict__ src, const uint32_t *__restrict__ idx, uint32_t n,
                          float *__restrict__ dst) {
@@ -664,6 +673,7 @@ int learner_create(spai_engine *e, int blocks, int hidden, const float *params, 
     };
     chk(L->p.alloc(n));
     chk(L->g.alloc(n));
+    chk(L->bsum.alloc(1));
     chk(L->m.alloc(n));
     chk(L->v.alloc(n));
     chk(L->wt.alloc((size_t)9 * 64 * 64));   // packed [k][n] conv weights (cin, cout <= 64)
@@ -702,7 +712,7 @@ void learner_destroy(spai_learner *L) {
     if (!L) return;
     if (L->eng) (void)hipStreamSynchronize(L->eng->stream);
     if (L->comm) (void)ncclCommDestroy((ncclComm_t)L->comm);
-    for (auto *b : {&L->p, &L->g, &L->m, &L->v, &L->wt, &L->x_in, &L->pi, &L->zv, &L->d0, &L->d1, &L->d2, &L->dlogits,
+    for (auto *b : {&L->p, &L->g, &L->bsum, &L->m, &L->v, &L->wt, &L->x_in, &L->pi, &L->zv, &L->d0, &L->d1, &L->d2, &L->dlogits,
                     &L->dpre, &L->loss_terms, &L->wpart, &L->bpart, &L->run_buf})
         b->release();
     L->run_idx.release();
@@ -795,13 +805,22 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
 
     SPAI_TRY(crc);
     // ---------------- cross-rank reduction + Adam
-    float gscale = 1.0f;
-    if (L->comm) {   // (a 1-rank communicator reduces to a copy)
+    // The global step's gradient is the mean over every rank's samples: each rank
+    // weights its own mean gradient by B / sum(B) (one 4-byte all-reduce first),
+    // then the gradients are summed.  Exact for unequal per-rank batches; a 1-rank
+    // communicator multiplies by 1 and reduces to a copy (bit-identical step).
+    const float gscale = 1.0f;
+    if (L->comm) {
+        k_set1<<<1, 1, 0, st>>>(L->bsum.p, (float)B);
+        if (ncclAllReduce(L->bsum.p, L->bsum.p, 1, ncclFloat32, ncclSum, (ncclComm_t)L->comm, st) != ncclSuccess) {
+            set_error("ncclAllReduce of the batch sizes failed");
+            return SPAI_ERR_DEVICE;
+        }
+        k_weight_grad<<<blocks_of(L->n_params), kThreads, 0, st>>>(G, L->n_params, (float)B, L->bsum.p);
         if (ncclAllReduce(G, G, L->n_params, ncclFloat32, ncclSum, (ncclComm_t)L->comm, st) != ncclSuccess) {
             set_error("ncclAllReduce of the gradients failed");
             return SPAI_ERR_DEVICE;
         }
-        gscale = 1.0f / (float)L->world;
     }
     L->step += 1;
     const double t = (double)L->step;
@@ -889,6 +908,20 @@ int learner_set_comm(spai_learner *L, int rank, int world, const uint8_t *id) {
     const ncclResult_t r = ncclCommInitRank(&c, world, uid, rank);
     SPAI_CHECK(r == ncclSuccess, SPAI_ERR_DEVICE, "ncclCommInitRank failed: %s", ncclGetErrorString(r));
     L->comm = c;
+    return SPAI_OK;
+}
+
+// weight refresh of data-parallel replicas: every rank's parameters (BN running
+// statistics included) become rank `root`'s, by one RCCL broadcast over xGMI
+int learner_broadcast(spai_learner *L, int root) {
+    SPAI_CHECK(root >= 0 && root < L->world, SPAI_ERR_INVALID, "broadcast root %d outside world %d", root, L->world);
+    if (!L->comm) return SPAI_OK;   // no communicator: a single replica
+    hipStream_t st = L->eng->stream;
+    if (ncclBroadcast(L->p.p, L->p.p, L->n_params, ncclFloat32, root, (ncclComm_t)L->comm, st) != ncclSuccess) {
+        set_error("ncclBroadcast of the parameters failed");
+        return SPAI_ERR_DEVICE;
+    }
+    SPAI_HIP(hipStreamSynchronize(st));
     return SPAI_OK;
 }
 

@@ -187,10 +187,17 @@ struct Plan {
 // into the zeroed 256-B block below the buffer, so the k-loop needs no select.  epi[t] is the
 // relative address of this lane's 4 output channels of co tile 0 at its
 // position (co tile c: epi ^ (c << 5)).
+// rel is stored biased by +256 (the zero block becomes 0..255) as 16-bit halves,
+// two taps per register (tap 2j low, 2j+1 high): 5 registers per tile instead of
+// 9, which lets the pair split hold 11 position tiles without spilling.
 template <int NT>
 struct Geo {
-    int rel[NT][9];
+    uint32_t rel2[NT][5];
     int epi[NT];
+    // B-fragment offset of tile t, tap `tap`, relative to (buffer - 256)
+    __device__ __forceinline__ uint32_t b(int t, int tap) const {
+        return (tap & 1) ? rel2[t][tap >> 1] >> 16 : rel2[t][tap >> 1] & 0xFFFFu;
+    }
 };
 
 template <int W, int CT, int NPT>
@@ -210,7 +217,9 @@ __device__ __forceinline__ void make_geo(int lane, Geo<Plan<W, CT, NPT>::NT> &g)
             const int full = r * 128 + ((q ^ (r & 7)) << 4);
             // an out-of-board tap reads the zero block below the buffer at the same
             // 16-B granule its row would use, so it never adds a bank conflict
-            g.rel[t][tap] = ok ? full : (full & 255) - 256;
+            const uint32_t v = (uint32_t)((ok ? full : (full & 255) - 256) + 256);
+            if (tap & 1) g.rel2[t][tap >> 1] |= v << 16;
+            else g.rel2[t][tap >> 1] = v;
         }
         g.epi[t] = p * 128 + ((((q >> 1)) ^ (p & 7)) << 4) + ((q & 1) << 3);
     }
@@ -262,7 +271,7 @@ __device__ __forceinline__ void conv_mfma(const uint8_t *smem, const Geo<Plan<W,
     for (int kb = 0; kb < DB - 1; ++kb) {
         const int tap = kb >> 1, flip = (kb & 1) << 6;
 #pragma unroll
-        for (int t = 0; t < NT; ++t) B[kb][t] = *(const uint4 *)(smem + IN + (g.rel[t][tap] ^ flip));
+        for (int t = 0; t < NT; ++t) B[kb][t] = *(const uint4 *)(smem + (IN - 256) + (g.b(t, tap) ^ flip));
     }
 #pragma unroll
     for (int ks = 0; ks < kKStepsRes; ++ks) {
@@ -288,7 +297,8 @@ __device__ __forceinline__ void conv_mfma(const uint8_t *smem, const Geo<Plan<W,
         if (ks + lb < kKStepsRes) {
             const int tap = (ks + lb) >> 1, flip = ((ks + lb) & 1) << 6;
 #pragma unroll
-            for (int t = 0; t < NT; ++t) B[(ks + lb) % DB][t] = *(const uint4 *)(smem + IN + (g.rel[t][tap] ^ flip));
+            for (int t = 0; t < NT; ++t)
+                B[(ks + lb) % DB][t] = *(const uint4 *)(smem + (IN - 256) + (g.b(t, tap) ^ flip));
         }
 #pragma unroll
         for (int i = 0; i < PL::n; ++i)
@@ -372,7 +382,7 @@ __device__ __forceinline__ void residual_mfma(const uint8_t *smem, const Geo<Pla
     uint4 b[PL::n];
 #pragma unroll
     for (int i = 0; i < PL::n; ++i)
-        b[i] = *(const uint4 *)(smem + OUT + (g.rel[PL::pt(i)][4] ^ ((PL::co(i) >> 1) << 6)));
+        b[i] = *(const uint4 *)(smem + (OUT - 256) + (g.b(PL::pt(i), 4) ^ ((PL::co(i) >> 1) << 6)));
 #pragma unroll
     for (int i = 0; i < PL::n; ++i)
         acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(id[PL::co(i) & 1]), as_bf16x8(b[i]), acc[i], 0, 0,
@@ -944,19 +954,12 @@ int ensure_io(spai_net *n, uint32_t cnt) {
     return SPAI_OK;
 }
 
-int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
-#ifndef SPAI_DIAG
-    (void)n;
-    (void)cycles;
-    SPAI_CHECK(false, SPAI_ERR_UNSUPPORTED, "phase stamps need the diagnostic build (make -C self-play-ai_amd diag)");
-#endif
-    SPAI_CHECK(cnt > 0, SPAI_ERR_INVALID, "need cnt > 0");
-    SPAI_CHECK(n->dtype == SPAI_DTYPE_BF16, SPAI_ERR_UNSUPPORTED, "phase stamps time the bf16 kernel");
-    SPAI_TRY(ensure_io(n, cnt));
-    hipStream_t st = n->eng->stream;
-    std::vector<uint64_t> m(cnt), t(cnt);
+// random reachable, ongoing positions (player-to-move view) for the forward benchmarks
+static void random_positions(uint32_t cnt, std::vector<uint64_t> &m, std::vector<uint64_t> &t) {
+    m.resize(cnt);
+    t.resize(cnt);
     uint64_t h = 0x1234;
-    for (uint32_t i = 0; i < cnt; ++i) {   // random reachable positions
+    for (uint32_t i = 0; i < cnt; ++i) {
         c4::State s{0, 0, 0, c4::kOngoing};
         h = c4::splitmix64(h);
         for (int k = 0, plies = (int)(h % 30); k < plies; ++k) {
@@ -971,9 +974,56 @@ int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
         m[i] = xm ? s.x : s.o;
         t[i] = xm ? s.o : s.x;
     }
+}
+
+// Device time of the search's forward launch alone (net_eval_batch with a
+// device-side leaf count, as in search) on `cnt` random positions: mean of
+// `iters` back-to-back launches between two HIP events on the engine stream.
+int net_bench(spai_net *n, uint32_t cnt, uint32_t iters, double *ms) {
+    SPAI_CHECK(cnt > 0 && iters > 0, SPAI_ERR_INVALID, "need cnt > 0 and iters > 0");
+    SPAI_TRY(ensure_io(n, cnt));
+    if (!n->io_count.p) SPAI_TRY(n->io_count.alloc(1));
+    hipStream_t st = n->eng->stream;
+    std::vector<uint64_t> m, t;
+    random_positions(cnt, m, t);
+    SPAI_HIP(hipMemcpyAsync(n->io_mine.p, m.data(), (size_t)cnt * 8, hipMemcpyHostToDevice, st));
+    SPAI_HIP(hipMemcpyAsync(n->io_theirs.p, t.data(), (size_t)cnt * 8, hipMemcpyHostToDevice, st));
+    SPAI_HIP(hipMemcpyAsync(n->io_count.p, &cnt, 4, hipMemcpyHostToDevice, st));
+    for (int w = 0; w < 3; ++w)
+        SPAI_TRY(net_eval_batch(n, st, n->io_count.p, cnt, n->io_mine.p, n->io_theirs.p, n->io_priors.p, n->io_value.p));
+    hipEvent_t a, b;
+    SPAI_HIP(hipEventCreate(&a));
+    SPAI_HIP(hipEventCreate(&b));
+    SPAI_HIP(hipEventRecord(a, st));
+    for (uint32_t i = 0; i < iters; ++i)
+        SPAI_TRY(net_eval_batch(n, st, n->io_count.p, cnt, n->io_mine.p, n->io_theirs.p, n->io_priors.p, n->io_value.p));
+    SPAI_HIP(hipEventRecord(b, st));
+    SPAI_HIP(hipEventSynchronize(b));
+    float f = 0;
+    SPAI_HIP(hipEventElapsedTime(&f, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    *ms = f / iters;
+    return SPAI_OK;
+}
+
+int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
+#ifndef SPAI_DIAG
+    (void)n;
+    (void)cycles;
+    SPAI_CHECK(false, SPAI_ERR_UNSUPPORTED, "phase stamps need the diagnostic build (make -C self-play-ai_amd diag)");
+#endif
+    SPAI_CHECK(cnt > 0, SPAI_ERR_INVALID, "need cnt > 0");
+    SPAI_CHECK(n->dtype == SPAI_DTYPE_BF16, SPAI_ERR_UNSUPPORTED, "phase stamps time the bf16 kernel");
+    SPAI_TRY(ensure_io(n, cnt));
+    hipStream_t st = n->eng->stream;
+    std::vector<uint64_t> m, t;
+    random_positions(cnt, m, t);
     const char *es = std::getenv("SPAI_PHASE_S");   // diagnostic: group size to time (default 8)
     const int S = es ? std::max(1, std::min(kS, std::atoi(es))) : kS;
-    const uint32_t grid = (cnt + S - 1) / S;
+    uint32_t grid = (cnt + S - 1) / S;
+    if (const char *eg = std::getenv("SPAI_PHASE_GRID"))   // fewer workgroups: the stamps keep each one's LAST group
+        grid = std::min<uint32_t>(grid, (uint32_t)std::max(1, std::atoi(eg)));
     DevBuf<unsigned long long> d;
     SPAI_TRY(d.alloc((size_t)grid * kWaves * kStamps));
     SPAI_HIP(hipMemsetAsync(d.p, 0, d.n * 8, st));

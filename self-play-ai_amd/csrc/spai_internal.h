@@ -143,6 +143,7 @@ struct spai_learner {
     std::vector<Conv> convs;            // stem, 2*blocks residual, policy head, value head
     size_t pol_w = 0, pol_b = 0, val_w = 0, val_b = 0;
     spai::DevBuf<float> p, g, m, v;     // params, grads, Adam moments (flat)
+    spai::DevBuf<float> bsum;           // data parallel: sum over ranks of the batch size
     spai::DevBuf<float> wt;             // flipped/transposed conv weights for the data gradient
     spai::DevBuf<float> x_in, pi, zv;   // batch
     std::vector<spai::DevBuf<float>> z, a, mean, invstd;   // per conv layer
@@ -199,6 +200,7 @@ int net_forward_x(spai_net *net, uint32_t n, const float *x, float *logits, floa
 int net_predict(spai_net *net, uint32_t n, const spai_c4_state *states, float *priors, float *values);
 size_t net_num_params(int game, int blocks, int hidden);
 int net_phase_stamps(spai_net *net, uint32_t n, double *cycles);
+int net_bench(spai_net *net, uint32_t n, uint32_t iters, double *ms);
 void net_init_params(int game, int blocks, int hidden, uint64_t seed, float *params);
 // evaluate `count` (device scalar) leaves of the batch; grid sized for max_n
 int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint32_t max_n,
@@ -219,6 +221,7 @@ int learner_params(spai_learner *l, float *params, size_t n, bool grads);
 int learner_train_epochs(spai_learner *l, uint32_t n, const float *states, const float *policies, const float *values,
                          uint32_t epochs, uint32_t batch, uint64_t seed, float *loss3);
 int learner_set_comm(spai_learner *l, int rank, int world, const uint8_t *id);
+int learner_broadcast(spai_learner *l, int root);
 int comm_unique_id(uint8_t *id);
 
 // interop.cpp

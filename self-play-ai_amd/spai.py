@@ -33,9 +33,9 @@ SYMBOLS = [
     "spai_net_destroy", "spai_net_forward", "spai_predict", "spai_engine_set_net", "spai_trees_create",
     "spai_tree_reset", "spai_search", "spai_tree_use_subtree", "spai_tree_node", "spai_tree_size",
     "spai_selfplay_run", "spai_engine_set_timing", "spai_engine_timing", "spai_engine_timing_items",
-    "spai_net_phase_cycles", "spai_adam_config_default", "spai_learner_create", "spai_learner_destroy",
+    "spai_net_phase_cycles", "spai_net_bench", "spai_adam_config_default", "spai_learner_create", "spai_learner_destroy",
     "spai_learner_train_batch", "spai_learner_params", "spai_learner_grads", "spai_comm_unique_id",
-    "spai_learner_set_comm", "spai_params_save_safetensors", "spai_params_load_safetensors",
+    "spai_learner_set_comm", "spai_learner_broadcast", "spai_params_save_safetensors", "spai_params_load_safetensors",
     "spai_replay_create", "spai_replay_destroy", "spai_replay_push", "spai_replay_pop", "spai_replay_size",
     "spai_choose_multiple", "spai_pipeline_config_default", "spai_pipeline_run", "spai_learner_train",
     "spai_policy_normalize", "spai_policy_best_action", "spai_policy_sample",
@@ -150,6 +150,7 @@ def lib():
         L.spai_engine_timing.argtypes = [vp, vp, vp]
         L.spai_engine_timing_items.argtypes = [vp, vp, vp]
         L.spai_net_phase_cycles.argtypes = [vp, u32, vp]
+        L.spai_net_bench.argtypes = [vp, u32, u32, vp]
         L.spai_adam_config_default.argtypes = [P(AdamConfig)]
         L.spai_learner_create.argtypes = [vp, i32, i32, vp, C.c_size_t, P(AdamConfig), P(vp)]
         L.spai_learner_destroy.argtypes = [vp]
@@ -159,6 +160,7 @@ def lib():
         L.spai_learner_train.argtypes = [vp, u32, vp, vp, vp, u32, u32, u64, vp]
         L.spai_comm_unique_id.argtypes = [vp]
         L.spai_learner_set_comm.argtypes = [vp, i32, i32, vp]
+        L.spai_learner_broadcast.argtypes = [vp, i32]
         L.spai_params_save_safetensors.argtypes = [i32, i32, i32, vp, C.c_size_t, C.c_char_p]
         L.spai_params_load_safetensors.argtypes = [i32, i32, i32, C.c_char_p, vp, C.c_size_t]
         L.spai_replay_create.argtypes = [u32, P(vp)]
@@ -245,6 +247,12 @@ class Net:
         c = np.zeros(20, np.float64)
         _check(lib().spai_net_phase_cycles(self.h, count, _p(c)))
         return c
+
+    def bench(self, count, iters=50):
+        """ms per forward launch alone on `count` random positions (spai_net_bench)"""
+        ms = np.zeros(1, np.float64)
+        _check(lib().spai_net_bench(self.h, count, iters, _p(ms)))
+        return float(ms[0])
 
     def predict(self, states):
         a = states_array(states)
@@ -453,6 +461,10 @@ class Learner:
     def set_comm(self, rank, world, uid=None):
         buf = None if uid is None else np.frombuffer(bytes(uid), np.uint8).copy()
         _check(lib().spai_learner_set_comm(self.h, rank, world, None if buf is None else _p(buf)))
+
+    def broadcast(self, root=0):
+        """RCCL broadcast of rank `root`'s parameters to every rank (weight refresh)"""
+        _check(lib().spai_learner_broadcast(self.h, root))
 
     def close(self):
         if self.h:

@@ -521,6 +521,34 @@ def test_learner_rccl_single_rank(spai):
     np.testing.assert_array_equal(out[0][1], out[1][1])
 
 
+def test_learner_rccl_weighting_and_broadcast(spai):
+    """the data-parallel step weights each rank's mean gradient by B / sum(B): on
+    a 1-rank communicator that weight is exactly 1 for any B (steps of 32 and 48
+    samples stay bit-identical to the plain steps); the RCCL broadcast of the
+    parameters (weight refresh) leaves a single replica unchanged"""
+    z = np.load(os.path.join(GOLDEN, "learner_c4_1x64.npz"))
+    blocks, hidden, seed, B, K = [int(v) for v in z["meta"]]
+    s = np.concatenate(list(z["states"]))
+    p = np.concatenate(list(z["policies"]))
+    v = np.concatenate(list(z["values"]))
+    out = []
+    for use_comm in (False, True):
+        e = spai.Engine(num_searches=1, max_trees=1)
+        L = spai.Learner(e, blocks, spai.init_params(blocks, hidden, seed=seed), hidden=hidden)
+        if use_comm:
+            L.set_comm(0, 1, spai.comm_unique_id())
+        l1 = L.train_batch(s[:32], p[:32], v[:32])
+        l2 = L.train_batch(s[32:80], p[32:80], v[32:80])
+        before = L.params()
+        L.broadcast(0)
+        np.testing.assert_array_equal(L.params(), before)
+        out.append((np.array([l1, l2]), before))
+        L.close()
+        e.close()
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
 # ------------------------------------------------------------------ pipeline
 def test_pipeline_concurrent(spai, tmp_path):
     """train_concurrent (main.rs:137-235) end to end on one GPU: a self-play worker
