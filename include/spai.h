@@ -361,7 +361,8 @@ typedef struct spai_chess_state {
 typedef struct spai_chess spai_chess;
 typedef struct spai_chess_net spai_chess_net;
 
-/* cfg.max_moves = longest game (sizes the transposition tables; default 2048) */
+/* cfg.max_moves = longest game (sizes the transposition tables).  Default 11,904: the
+ * fifty-move rule bounds a game at 11,898 plies, so the default never overflows. */
 int spai_chess_config_default(spai_config *cfg);
 int spai_chess_create(const spai_config *cfg, int device, spai_chess **out);
 int spai_chess_destroy(spai_chess *e);

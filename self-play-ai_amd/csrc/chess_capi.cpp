@@ -84,7 +84,11 @@ int spai_chess_config_default(spai_config *cfg) {
     cfg->num_searches = 400;    // BASELINE config 4 (chess, 400 sims/move)
     cfg->temperature = 1.25f;   // learner_concurrent.rs:53
     cfg->max_trees = 1024;      // BASELINE config 4 (1024 parallel games)
-    cfg->max_moves = 2048;      // longest game: transposition table entries
+    // longest game: transposition-table entries per game.  The reference's rules end a
+    // game by the fifty-move counter (chess.rs:124-144,154-166: a draw at 100 plies with
+    // no pawn move, capture or castle-right change), which bounds any game at 5,949
+    // moves = 11,898 plies; 11,904 entries (93 KB per game) can therefore never overflow.
+    cfg->max_moves = 11904;
     cfg->eval = SPAI_EVAL_NET;
     cfg->seed = 0;
     return SPAI_OK;

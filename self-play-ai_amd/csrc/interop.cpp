@@ -5,13 +5,14 @@
 // every variable by its path name on the root path; a name already present
 // gets the suffix "__<number of variables in the store>" (nn::Path::add).
 // Construction order (model/mod.rs:167-184, model/connect_four.rs:54-72,
-// model/tictactoe.rs:54-72, model/chess.rs:48-70):
-// each conv2d adds weight, bias; each batch_norm2d weight, bias, running_mean,
-// running_var; each linear weight, bias — stem, residual blocks, policy head,
-// value head.  tch is not vendored: this naming is restated from its source as
-// recalled (parity unpinned); the file format itself is checked against the
-// safetensors package in the tests.
-//
+// model/tictactoe.rs:54-72, model/chess.rs:48-70): stem, residual blocks,
+// policy head, value head.  The variable-creation order INSIDE each tch module
+// decides every "__N" suffix; it is the one table below (kModuleOrder).  tch is
+// not vendored, so that table is restated from tch 0.13's nn/conv.rs,
+// nn/linear.rs and nn/batch_norm.rs as recalled: PARITY UNPINNED -- no
+// tch-written checkpoint exists here to check it against.  The file format
+// itself is checked against the safetensors package in the tests, and the
+// loader names the first tensor it cannot match (name, shape or dtype).
 // File format: u64 little-endian header length, a JSON header
 // {"name": {"dtype": "F32", "shape": [...], "data_offsets": [begin, end]}, ...}
 // and the raw little-endian tensor bytes.
@@ -33,38 +34,56 @@ struct TensorSpec {
     size_t count;
 };
 
-// A net's variables in construction order, with tch names and shapes.
+// Variable-creation order inside one tch module (the single place to correct if
+// a real tch checkpoint disagrees).  The flat parameter vector of spai_net_create
+// always stores weight before bias; only the names follow this order.
+struct ModuleOrder {
+    bool conv_bias_first;     // nn::conv2d: `bias` var created before `weight`
+    bool linear_bias_first;   // nn::linear: `bias` var created before `weight`
+    // nn::batch_norm2d: weight, bias, running_mean, running_var (fixed)
+};
+constexpr ModuleOrder kModuleOrder{true, true};
+
+// A net's variables in flat order, with tch names (VarStore: a repeated name gets
+// "__<variables created so far>", nn::Path::add) and shapes.
 struct SpecBuilder {
     std::vector<TensorSpec> out;
     std::map<std::string, int> seen;
-    size_t off = 0;
-    void add(const std::string &base, std::vector<int64_t> shape) {
+    size_t created = 0;   // variables created so far (tch's suffix counter)
+    size_t off = 0;       // flat offset
+    std::string name(const std::string &base) {
+        std::string n = seen.count(base) ? base + "__" + std::to_string(created) : base;
+        seen[base] = 1;
+        ++created;
+        return n;
+    }
+    void push(const std::string &nm, std::vector<int64_t> shape) {
         size_t n = 1;
         for (int64_t d : shape) n *= (size_t)d;
-        std::string name = base;
-        if (seen.count(base)) name = base + "__" + std::to_string(out.size());
-        seen[base] = 1;
-        out.push_back({name, shape, off, n});
+        out.push_back({nm, shape, off, n});
         off += n;
     }
-    void conv(int64_t ci, int64_t co, int64_t k) {   // nn::conv2d: weight, bias
-        add("weight", {co, ci, k, k});
-        add("bias", {co});
+    void weight_bias(bool bias_first, std::vector<int64_t> wshape, int64_t nb) {
+        std::string w, b;
+        if (bias_first) {
+            b = name("bias");
+            w = name("weight");
+        } else {
+            w = name("weight");
+            b = name("bias");
+        }
+        push(w, wshape);   // flat order: weight, bias
+        push(b, {nb});
     }
-    void bn(int64_t c) {                              // nn::batch_norm2d
-        add("weight", {c});
-        add("bias", {c});
-        add("running_mean", {c});
-        add("running_var", {c});
+    void conv(int64_t ci, int64_t co, int64_t k) { weight_bias(kModuleOrder.conv_bias_first, {co, ci, k, k}, co); }
+    void bn(int64_t c) {
+        for (const char *v : {"weight", "bias", "running_mean", "running_var"}) push(name(v), {c});
     }
     void conv_bn(int64_t ci, int64_t co) {
         conv(ci, co, 3);
         bn(co);
     }
-    void linear(int64_t in, int64_t outf) {           // nn::linear: weight [out][in], bias
-        add("weight", {outf, in});
-        add("bias", {outf});
-    }
+    void linear(int64_t in, int64_t outf) { weight_bias(kModuleOrder.linear_bias_first, {outf, in}, outf); }
 };
 
 // Connect4 (model/connect_four.rs:50-72) and TicTacToe (model/tictactoe.rs:50-72):
@@ -266,13 +285,27 @@ int params_load_safetensors(int game, int blocks, int hidden, const char *path, 
         } while (js.ok && js.eat(','));
         SPAI_CHECK(js.ok && js.eat('}'), SPAI_ERR_INVALID, "%s: bad header", path);
     }
+    auto shape_str = [](const std::vector<int64_t> &v) {
+        std::string r = "[";
+        for (size_t i = 0; i < v.size(); ++i) r += (i ? "," : "") + std::to_string(v[i]);
+        return r + "]";
+    };
     for (const TensorSpec &t : specs) {
         auto it = entries.find(t.name);
-        SPAI_CHECK(it != entries.end(), SPAI_ERR_INVALID, "%s: missing tensor '%s'", path, t.name.c_str());
+        if (it == entries.end()) {   // name the first mismatch, with a same-shape candidate if any
+            std::string cand;
+            for (const auto &kv : entries)
+                if (kv.second.shape == t.shape && !cand.size()) cand = kv.first;
+            SPAI_CHECK(false, SPAI_ERR_INVALID,
+                       "%s: missing tensor '%s' %s (tch naming is restated, parity unpinned; the file has %zu "
+                       "tensors%s%s%s)", path, t.name.c_str(), shape_str(t.shape).c_str(), entries.size(),
+                       cand.size() ? ", same shape: '" : "", cand.c_str(), cand.size() ? "'" : "");
+        }
         const Entry &e = it->second;
         SPAI_CHECK(e.dtype == "F32", SPAI_ERR_UNSUPPORTED, "%s: tensor '%s' is %s, expected F32", path,
                    t.name.c_str(), e.dtype.c_str());
-        SPAI_CHECK(e.shape == t.shape, SPAI_ERR_INVALID, "%s: tensor '%s' has the wrong shape", path, t.name.c_str());
+        SPAI_CHECK(e.shape == t.shape, SPAI_ERR_INVALID, "%s: tensor '%s' has shape %s, expected %s", path,
+                   t.name.c_str(), shape_str(e.shape).c_str(), shape_str(t.shape).c_str());
         SPAI_CHECK(e.begin >= 0 && e.end - e.begin == (int64_t)(4 * t.count) && (size_t)e.end <= data_len,
                    SPAI_ERR_INVALID, "%s: tensor '%s' has bad data offsets", path, t.name.c_str());
         memcpy(params + t.offset, data + e.begin, 4 * t.count);   // little-endian F32 on this host

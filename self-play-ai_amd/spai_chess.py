@@ -119,11 +119,13 @@ def states_from(boards):
 
 class ChessEngine:
     def __init__(self, num_searches=400, max_trees=1024, eval_kind=EVAL_NET, device=0, c=2.0, temperature=1.25,
-                 seed=0, max_moves=2048):
+                 seed=0, max_moves=None):
         cfg = Config()
         _check(lib().spai_chess_config_default(C.byref(cfg)))
         cfg.c, cfg.num_searches, cfg.temperature = c, num_searches, temperature
-        cfg.max_trees, cfg.max_moves, cfg.eval, cfg.seed = max_trees, max_moves, eval_kind, seed
+        cfg.max_trees, cfg.eval, cfg.seed = max_trees, eval_kind, seed
+        if max_moves is not None:
+            cfg.max_moves = max_moves
         self.cfg = cfg
         h = C.c_void_p()
         _check(lib().spai_chess_create(C.byref(cfg), device, C.byref(h)))

@@ -1,8 +1,9 @@
 """safetensors checkpoints with tch VarStore naming, host-only.
 
 The file format is checked against the official `safetensors` package (read
-and write); the tch naming (root-path names, "__<count>" suffix on repeats)
-is restated from tch 0.13, which is not vendored: parity unpinned."""
+and write); the tch naming (root-path names, "__<count>" suffix on repeats,
+conv/linear create `bias` before `weight`: interop.cpp kModuleOrder) is
+restated from tch 0.13, which is not vendored: parity unpinned."""
 import os
 
 import numpy as np
@@ -12,27 +13,32 @@ spai = pytest.importorskip("spai")
 st = pytest.importorskip("safetensors.numpy")
 
 
-def expected_names(blocks):
+def tch_names(modules):
+    """flat-order names for a list of modules ("conv", "bn", "linear"): tch creates
+    conv/linear `bias` before `weight` (the suffix counts variables created so
+    far); the flat vector stores weight before bias"""
     names, seen = [], set()
 
-    def add(base):
-        names.append(base + "__%d" % len(names) if base in seen else base)
+    def name(base):
+        n = base + "__%d" % created[0] if base in seen else base
         seen.add(base)
+        created[0] += 1
+        return n
 
-    def conv_bn():
-        for b in ("weight", "bias", "weight", "bias", "running_mean", "running_var"):
-            add(b)
-
-    conv_bn()
-    for _ in range(2 * blocks):
-        conv_bn()
-    conv_bn()
-    add("weight")
-    add("bias")
-    conv_bn()
-    add("weight")
-    add("bias")
+    created = [0]
+    for m in modules:
+        if m == "bn":
+            names += [name(v) for v in ("weight", "bias", "running_mean", "running_var")]
+        else:
+            b = name("bias")
+            w = name("weight")
+            names += [w, b]
     return names
+
+
+def expected_names(blocks):
+    """stem + 2*blocks residual convs (conv, BN), policy head (conv, BN, linear), value head"""
+    return tch_names(["conv", "bn"] * (1 + 2 * blocks) + ["conv", "bn", "linear", "conv", "bn", "linear"])
 
 
 @pytest.mark.parametrize("blocks", [0, 2, 6])
@@ -47,7 +53,8 @@ def test_safetensors_roundtrip_and_format(tmp_path, blocks):
     assert set(t) == set(names)
     flat = np.concatenate([t[n].reshape(-1) for n in names])
     np.testing.assert_array_equal(flat, p)
-    assert t["weight"].shape == (64, 3, 3, 3)                 # stem conv
+    assert t["weight"].shape == (64, 3, 3, 3) and t["bias"].shape == (64,)   # stem conv (bias created first)
+    assert names[:6] == ["weight", "bias", "weight__2", "bias__3", "running_mean", "running_var"]
     assert t["running_var"].shape == (64,)
     last_lin = names[-2]
     assert t[last_lin].shape == (1, 126)                       # value head linear
@@ -111,11 +118,7 @@ def test_safetensors_ttt_and_chess_nets(tmp_path):
     spai.save_params(path, p, blocks, hidden=256, game=spai.GAME_CHESS)
     np.testing.assert_array_equal(spai.load_params(path, blocks, hidden=256, game=spai.GAME_CHESS, n=p.size), p)
     t = st.load_file(path)
-    names, seen = [], set()
-    for base in (["weight", "bias", "weight", "bias", "running_mean", "running_var"] * (1 + 2 * blocks) +
-                 ["weight", "bias"] * 5):
-        names.append(base + "__%d" % len(names) if base in seen else base)
-        seen.add(base)
+    names = tch_names(["conv", "bn"] * (1 + 2 * blocks) + ["conv"] * 3 + ["linear"] * 2)
     assert set(t) == set(names)
     np.testing.assert_array_equal(np.concatenate([t[n].reshape(-1) for n in names]), p)
     shapes = [t[n].shape for n in names]
