@@ -174,8 +174,8 @@ int spai_engine_destroy(spai_engine *e) {
     T.root_status.release();
     T.path.release();
     T.depth.release();
+    T.slot.release();
     for (Batch &B : e->batch) {
-        B.count.release();
         B.tree.release();
         B.mine.release();
         B.theirs.release();

@@ -2,15 +2,24 @@
 // (learner_concurrent.rs:169-242).
 //
 // Trees live in HBM as per-tree arenas of 16-B node records (spai_internal.h).
-// One search iteration (mcts.rs:214-285) is three launches on the engine stream:
-//   k_select        8 lanes per tree (one per child slot): PUCT descent from
-//                   the root, state replayed on bitboards, leaf terminal check;
-//                   terminal leaves are backed up in place, live leaves are
-//                   appended to the batch (wave-aggregated atomic slot).
-//   evaluate        the fused ResNet forward (net_c4.hip) or a stub evaluator.
-//   k_expand        8 lanes per leaf: legal moves by ballot, children packed by
-//                   a per-leaf prefix count, priors written, value backed up
-//                   along the recorded path (lanes split the levels).
+// One search iteration (mcts.rs:214-285) is two launches per search chain:
+//   evaluate        the fused ResNet forward (net_c4.hip) or a stub evaluator
+//                   over this iteration's leaf batch;
+//   k_expand_select per tree, 8 lanes (one per child slot): expand the tree's
+//                   leaf of this iteration if it had one (legal moves by
+//                   ballot, children packed by a prefix count, priors written,
+//                   value backed up along the recorded path, lanes splitting
+//                   the levels), then the NEXT iteration's PUCT descent from
+//                   the root (state replayed on bitboards, leaf terminal check;
+//                   terminal leaves backed up in place, live leaves appended to
+//                   the next batch).
+// Trees are independent, so expanding tree t and selecting tree t again in one
+// launch is the reference's per-tree order (expand+backprop of iteration i,
+// then select of i+1) and the results are those of separate launches; the
+// fusion removes one kernel boundary from every iteration's critical path.
+// The first iteration starts with k_select alone, the last ends with k_expand.
+// Leaf batches are double-buffered by iteration parity, and every iteration
+// has its own slot counter (zeroed once per search call).
 // The host only sees the trees between moves: root visit counts come back once
 // per search call, the sampled child goes down as the new root.
 #include <algorithm>
@@ -39,7 +48,9 @@ struct TreeView {
     const uint8_t *root_n, *root_status;
     uint32_t *path;
     uint8_t *depth;
+    uint32_t *slot;   // the tree's leaf slot in the current batch, kNoSlot if terminal
 };
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
 struct BatchView {
     uint32_t *count;
@@ -74,15 +85,11 @@ __device__ __forceinline__ void backup(uint4 *nodes, const uint32_t *path, int d
     for (int lvl = lane8; lvl <= d; lvl += kLanesPerTree) backup_level(nodes, path[lvl], d, lvl, v);
 }
 
-__global__ __launch_bounds__(kBlock) void k_select(TreeView T, BatchView B, const uint32_t *__restrict__ active,
-                                                   uint32_t n_active, float c, uint32_t *err) {
-    const uint32_t gi = (blockIdx.x * blockDim.x + threadIdx.x) / kLanesPerTree;
-#ifdef SPAI_TREE_PRIO
-    __builtin_amdgcn_s_setprio(SPAI_TREE_PRIO);   // experiment: issue priority against the co-resident forward
-#endif
-    const int lane8 = threadIdx.x & (kLanesPerTree - 1);
-    if (gi >= n_active) return;
-    const uint32_t t = active[gi];
+// PUCT descent of tree t (mcts.rs:235-250) by its 8 lanes; a live leaf gets a
+// slot in batch B (recorded in T.slot[t]), a terminal leaf is backed up in place
+__device__ __forceinline__ void select_tree(const TreeView &T, const BatchView &B, uint32_t t, int lane8, float c,
+                                            uint32_t *err) {
+    if (lane8 == 0) T.slot[t] = kNoSlot;
     uint4 *nodes = T.nodes + (size_t)t * T.cap;
     uint32_t *path = T.path + (size_t)t * kMaxDepth;
     uint32_t node = T.root[t];
@@ -162,40 +169,19 @@ __global__ __launch_bounds__(kBlock) void k_select(TreeView T, BatchView B, cons
         return;
     }
     // live leaf -> batch slot (mcts.rs:249-250)
-    uint32_t slot = 0;
-    if (lane8 == 0) slot = atomicAdd(B.count, 1u);
-    slot = __shfl(slot, 0, kLanesPerTree);
     if (lane8 == 0) {
+        const uint32_t slot = atomicAdd(B.count, 1u);
         const bool xm = c4::x_to_move(n);
+        T.slot[t] = slot;
         B.tree[slot] = t;
         B.mine[slot] = xm ? x : o;
         B.theirs[slot] = xm ? o : x;
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_eval_stub(BatchView B, uint32_t max_n, int kind) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= max_n || s >= *B.count) return;
-    // hash evaluator keys on absolute X/O stones: recover them from the player-to-move view
-    const uint32_t n = (uint32_t)c4::popc64(B.mine[s] | B.theirs[s]);
-    const bool xm = (n & 1u) == 0;
-    const uint64_t x = xm ? B.mine[s] : B.theirs[s], o = xm ? B.theirs[s] : B.mine[s];
-    float pr[c4::kActions], v;
-    c4::stub_eval(kind, x, o, (uint8_t)n, pr, &v);
-    for (int a = 0; a < c4::kActions; ++a) B.priors[(size_t)s * kPriorStride + a] = pr[a];
-    B.value[s] = v;
-}
-
-__global__ __launch_bounds__(kBlock) void k_expand(TreeView T, BatchView B, uint32_t max_n, uint32_t *err,
-                                                   uint32_t *iter_count, uint32_t *next_count) {
-    const uint32_t s = (blockIdx.x * blockDim.x + threadIdx.x) / kLanesPerTree;
-    const int lane8 = threadIdx.x & (kLanesPerTree - 1);
-    const uint32_t count = *B.count;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        *iter_count = count;   // per-iteration evaluated leaves
-        *next_count = 0u;      // the next iteration's batch counter (double-buffered)
-    }
-    if (s >= max_n || s >= count) return;
+// expand leaf slot s of batch B (mcts.rs:116-143) and back its value up (:145-159)
+__device__ __forceinline__ void expand_leaf(const TreeView &T, const BatchView &B, uint32_t s, int lane8,
+                                            uint32_t *err) {
     const uint32_t t = B.tree[s];
     uint4 *nodes = T.nodes + (size_t)t * T.cap;
     const uint32_t *path = T.path + (size_t)t * kMaxDepth;
@@ -222,6 +208,55 @@ __global__ __launch_bounds__(kBlock) void k_expand(TreeView T, BatchView B, uint
     backup(nodes, path, d, B.value[s], lane8);
 }
 
+__global__ __launch_bounds__(kBlock) void k_select(TreeView T, BatchView B, const uint32_t *__restrict__ active,
+                                                   uint32_t n_active, float c, uint32_t *err) {
+    const uint32_t gi = (blockIdx.x * blockDim.x + threadIdx.x) / kLanesPerTree;
+#ifdef SPAI_TREE_PRIO
+    __builtin_amdgcn_s_setprio(SPAI_TREE_PRIO);   // experiment: issue priority against the co-resident forward
+#endif
+    if (gi >= n_active) return;
+    select_tree(T, B, active[gi], threadIdx.x & (kLanesPerTree - 1), c, err);
+}
+
+// expand this iteration's leaf of every tree (batch `cur`), then select the next
+// iteration's leaf into batch `nxt`.  A tree's lanes are one group of 8 in one
+// wave: its expand stores are made visible to its own select loads by a
+// workgroup-scope fence (vmcnt(0); the CU's L1 is coherent within a workgroup).
+__global__ __launch_bounds__(kBlock) void k_expand_select(TreeView T, BatchView cur, BatchView nxt,
+                                                          const uint32_t *__restrict__ active, uint32_t n_active,
+                                                          float c, uint32_t *err) {
+    const uint32_t gi = (blockIdx.x * blockDim.x + threadIdx.x) / kLanesPerTree;
+#ifdef SPAI_TREE_PRIO
+    __builtin_amdgcn_s_setprio(SPAI_TREE_PRIO);
+#endif
+    if (gi >= n_active) return;
+    const int lane8 = threadIdx.x & (kLanesPerTree - 1);
+    const uint32_t t = active[gi];
+    const uint32_t s = T.slot[t];
+    if (s != kNoSlot) expand_leaf(T, cur, s, lane8, err);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    select_tree(T, nxt, t, lane8, c, err);
+}
+
+__global__ __launch_bounds__(kBlock) void k_eval_stub(BatchView B, uint32_t max_n, int kind) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= max_n || s >= *B.count) return;
+    // hash evaluator keys on absolute X/O stones: recover them from the player-to-move view
+    const uint32_t n = (uint32_t)c4::popc64(B.mine[s] | B.theirs[s]);
+    const bool xm = (n & 1u) == 0;
+    const uint64_t x = xm ? B.mine[s] : B.theirs[s], o = xm ? B.theirs[s] : B.mine[s];
+    float pr[c4::kActions], v;
+    c4::stub_eval(kind, x, o, (uint8_t)n, pr, &v);
+    for (int a = 0; a < c4::kActions; ++a) B.priors[(size_t)s * kPriorStride + a] = pr[a];
+    B.value[s] = v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_expand(TreeView T, BatchView B, uint32_t max_n, uint32_t *err) {
+    const uint32_t s = (blockIdx.x * blockDim.x + threadIdx.x) / kLanesPerTree;
+    if (s >= max_n || s >= *B.count) return;
+    expand_leaf(T, B, s, threadIdx.x & (kLanesPerTree - 1), err);
+}
+
 // per active tree: [0] = root first|nch<<24 (children word), [1..7] child visit counts
 __global__ void k_root_stats(TreeView T, const uint32_t *__restrict__ active, uint32_t n_active, uint32_t *out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -245,12 +280,15 @@ __global__ void k_trees_init(TreeView T, uint32_t first_tree, uint32_t n) {
 TreeView tree_view(spai_engine *e) {
     Trees &T = e->trees;
     return TreeView{T.nodes.p, T.cap, T.root.p, T.next_free.p, T.root_x.p, T.root_o.p, T.root_n.p, T.root_status.p,
-                    T.path.p, T.depth.p};
+                    T.path.p, T.depth.p, T.slot.p};
 }
 
-BatchView batch_view(spai_engine *e, int chain, uint32_t slot) {
+// chain `chain`'s leaf batch of search iteration `it`: buffers by parity, counter per iteration
+BatchView batch_view(spai_engine *e, int chain, uint32_t it) {
     Batch &B = e->batch[chain];
-    return BatchView{B.count.p + slot, B.tree.p, B.mine.p, B.theirs.p, B.priors.p, B.value.p};
+    const size_t h = (size_t)(it & 1u) * B.cap;
+    return BatchView{B.iter_counts.p + it, B.tree.p + h, B.mine.p + h, B.theirs.p + h,
+                     B.priors.p + h * kPriorStride, B.value.p + h};
 }
 
 // Number of search chains for n trees: two halves when each half still fills
@@ -356,15 +394,15 @@ int trees_create(spai_engine *e, uint32_t n) {
         SPAI_TRY(T.root_status.alloc(n));
         SPAI_TRY(T.path.alloc((size_t)n * kMaxDepth));
         SPAI_TRY(T.depth.alloc(n));
+        SPAI_TRY(T.slot.alloc(n));
         SPAI_TRY(e->active.alloc(n));
         SPAI_TRY(e->stats.alloc((size_t)n * 8));
-        for (Batch &B : e->batch) {   // one leaf batch per search chain
-            SPAI_TRY(B.count.alloc(2));
-            SPAI_TRY(B.tree.alloc(n));
-            SPAI_TRY(B.mine.alloc(n));
-            SPAI_TRY(B.theirs.alloc(n));
-            SPAI_TRY(B.priors.alloc((size_t)n * kPriorStride));
-            SPAI_TRY(B.value.alloc(n));
+        for (Batch &B : e->batch) {   // one double-buffered leaf batch per search chain
+            SPAI_TRY(B.tree.alloc(2 * (size_t)n));
+            SPAI_TRY(B.mine.alloc(2 * (size_t)n));
+            SPAI_TRY(B.theirs.alloc(2 * (size_t)n));
+            SPAI_TRY(B.priors.alloc(2 * (size_t)n * kPriorStride));
+            SPAI_TRY(B.value.alloc(2 * (size_t)n));
             B.cap = n;
         }
         T.n_trees = n;
@@ -415,10 +453,10 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
         off[h] = (uint32_t)((uint64_t)n * h / nchain);
         cnt[h] = (uint32_t)((uint64_t)n * (h + 1) / nchain) - off[h];
     }
-    for (int h = 0; h < nchain; ++h) {
+    for (int h = 0; h < nchain; ++h) {   // per-iteration leaf counters (also the batch slot counters)
         Batch &B = e->batch[h];
         if (B.iter_counts.n < num_searches) SPAI_TRY(B.iter_counts.alloc(std::max<uint32_t>(num_searches, 1)));
-        SPAI_HIP(hipMemsetAsync(B.count.p, 0, 8, st));
+        SPAI_HIP(hipMemsetAsync(B.iter_counts.p, 0, (size_t)std::max<uint32_t>(num_searches, 1) * 4, st));
     }
     SPAI_HIP(hipMemcpyAsync(e->active.p, tree_idx, n * 4, hipMemcpyHostToDevice, st));
     SPAI_HIP(hipMemsetAsync(e->err.p, 0, 4, st));
@@ -428,28 +466,39 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
     }
     const TreeView tv = tree_view(e);
     const bool timed = e->timer.enabled;   // samples every chain's launches every stride-th iteration
+    // per chain: select(0); then per iteration: evaluate(it), expand(it)+select(it+1)
+    // fused, and expand alone after the last evaluation.  Timer 0 samples the
+    // select-bearing launch (k_select / k_expand_select), 2 the last k_expand.
     for (uint32_t it = 0; it < num_searches; ++it) {
-        const uint32_t cur = it & 1u;
         for (int h = 0; h < nchain; ++h) {
             const hipStream_t sh = e->chain_stream[h];
-            Batch &B = e->batch[h];
-            const BatchView bv = batch_view(e, h, cur);
+            const BatchView bv = batch_view(e, h, it);
             const uint32_t nh = cnt[h], g8 = (nh + kTreesPerBlock - 1) / kTreesPerBlock;
             const uint32_t *act = e->active.p + off[h];
             const bool sample = timed && (it % e->timer.stride == 0);
-            if (sample) SPAI_TRY(timer_record(e, 0, it, true, sh, h));
-            k_select<<<g8, kBlock, 0, sh>>>(tv, bv, act, nh, e->cfg.c, e->err.p);
-            if (sample) SPAI_TRY(timer_record(e, 0, it, false, sh, h));
+            if (it == 0) {
+                if (sample) SPAI_TRY(timer_record(e, 0, it, true, sh, h));
+                k_select<<<g8, kBlock, 0, sh>>>(tv, bv, act, nh, e->cfg.c, e->err.p);
+                if (sample) SPAI_TRY(timer_record(e, 0, it, false, sh, h));
+            }
             if (sample) SPAI_TRY(timer_record(e, 1, it, true, sh, h));
             if (kind == SPAI_EVAL_NET) {
-                SPAI_TRY(net_eval_batch(e->net, sh, bv.count, nh, B.mine.p, B.theirs.p, B.priors.p, B.value.p));
+                SPAI_TRY(net_eval_batch(e->net, sh, bv.count, nh, bv.mine, bv.theirs, bv.priors, bv.value));
             } else {
                 k_eval_stub<<<(nh + kBlock - 1) / kBlock, kBlock, 0, sh>>>(bv, nh, kind);
             }
             if (sample) SPAI_TRY(timer_record(e, 1, it, false, sh, h));
-            if (sample) SPAI_TRY(timer_record(e, 2, it, true, sh, h));
-            k_expand<<<g8, kBlock, 0, sh>>>(tv, bv, nh, e->err.p, B.iter_counts.p + it, B.count.p + (cur ^ 1u));
-            if (sample) SPAI_TRY(timer_record(e, 2, it, false, sh, h));
+            if (it + 1 < num_searches) {
+                const bool s2 = timed && ((it + 1) % e->timer.stride == 0);
+                if (s2) SPAI_TRY(timer_record(e, 0, it + 1, true, sh, h));
+                k_expand_select<<<g8, kBlock, 0, sh>>>(tv, bv, batch_view(e, h, it + 1), act, nh, e->cfg.c,
+                                                       e->err.p);
+                if (s2) SPAI_TRY(timer_record(e, 0, it + 1, false, sh, h));
+            } else {
+                if (sample) SPAI_TRY(timer_record(e, 2, it, true, sh, h));
+                k_expand<<<g8, kBlock, 0, sh>>>(tv, bv, nh, e->err.p);
+                if (sample) SPAI_TRY(timer_record(e, 2, it, false, sh, h));
+            }
         }
     }
     SPAI_HIP(hipGetLastError());

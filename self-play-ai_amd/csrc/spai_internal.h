@@ -81,6 +81,7 @@ struct Trees {
     DevBuf<uint8_t> root_n, root_status;
     DevBuf<uint32_t> path;          // [n_trees * kMaxDepth]
     DevBuf<uint8_t> depth;          // [n_trees]
+    DevBuf<uint32_t> slot;          // [n_trees] leaf slot in the current batch (select -> expand)
     // host mirrors of the root bookkeeping
     std::vector<uint32_t> h_root;
     std::vector<c4::State> h_root_state;
@@ -88,10 +89,10 @@ struct Trees {
     std::vector<uint8_t> h_root_nch;
 };
 
-// One search iteration's leaf batch (the evaluator's input/output).
+// A search chain's leaf batches (the evaluator's input/output), double-buffered
+// by iteration parity: [2][cap] slots; iter_counts[it] is iteration it's slot counter.
 struct Batch {
     uint32_t cap = 0;
-    DevBuf<uint32_t> count;         // [1]
     DevBuf<uint32_t> tree;          // slot -> tree
     DevBuf<uint64_t> mine, theirs;  // leaf position, player-to-move view
     DevBuf<float> priors;           // [cap][8] masked softmax
