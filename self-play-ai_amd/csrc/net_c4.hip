@@ -1053,7 +1053,7 @@ int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
 }
 
 int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint32_t max_n, const uint64_t *mine,
-                   const uint64_t *theirs, float *priors, float *value) {
+                   const uint64_t *theirs, float *priors, float *value, uint32_t grid_cap_call) {
     if (!max_n) return SPAI_OK;
     if (net->dtype == SPAI_DTYPE_F32) return net_f32_launch(net, st, d_count, max_n, mine, theirs, nullptr, priors, value, nullptr);
     // SPAI_FWD_GRID caps the persistent grid (tuning knob: fewer workgroups -> larger groups S)
@@ -1063,6 +1063,7 @@ int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint3
     }();
     uint32_t grid = std::min<uint32_t>(max_n, (uint32_t)net->n_cu);
     if (grid_cap) grid = std::min(grid, grid_cap);
+    if (grid_cap_call) grid = std::min(grid, grid_cap_call);
     k_forward<false><<<grid, kThreads, 0, st>>>(d_count, max_n, 0, mine, theirs, nullptr, params_of(net), priors,
                                                 value, nullptr);
     SPAI_HIP(hipGetLastError());

@@ -298,14 +298,29 @@ BatchView batch_view(spai_engine *e, int chain, uint32_t it) {
 // kMinChainLeaves leaves per iteration.  (SPAI_CHAINS=k forces up to k chains,
 // for A/B measurements.)  The split never changes results: trees are independent.
 constexpr double kMinChainLeaves = 64;
-int chains_for(uint32_t n, double last_evals_per_iter) {
-    static const int forced = [] {
-        const char *v = std::getenv("SPAI_CHAINS");
-        return v ? std::max(1, std::min(spai_engine::kChains, std::atoi(v))) : 0;
-    }();
-    if (forced) return std::max(1, std::min<int>(forced, (int)(n / 64)));
-    if (last_evals_per_iter >= 0 && last_evals_per_iter < kMinChainLeaves) return 1;
-    return std::max(1, std::min<int>(2, (int)(n / 64)));
+static int env_int(const char *name, int dflt) {
+    const char *v = std::getenv(name);
+    return v ? std::atoi(v) : dflt;
+}
+// Mid-game policy (tuning knobs, off by default): when the previous search call
+// averaged fewer than SPAI_MID_LEAVES leaves per iteration (but at least
+// kMinChainLeaves), run SPAI_MID_CHAINS chains whose forwards are capped at
+// SPAI_MID_GRID workgroups, so that small per-chain batches run as larger groups
+// side by side on disjoint CUs instead of one after the other over all CUs.
+struct ChainPolicy {
+    int chains;
+    uint32_t grid_cap;   // 0: no cap
+};
+ChainPolicy chains_for(uint32_t n, double last_evals_per_iter) {
+    static const int forced = std::max(0, std::min(spai_engine::kChains, env_int("SPAI_CHAINS", 0)));
+    static const int mid_leaves = env_int("SPAI_MID_LEAVES", 0);
+    static const int mid_chains = std::max(1, std::min(spai_engine::kChains, env_int("SPAI_MID_CHAINS", 2)));
+    static const uint32_t mid_grid = (uint32_t)std::max(0, env_int("SPAI_MID_GRID", 0));
+    if (forced) return {std::max(1, std::min<int>(forced, (int)(n / 64))), 0u};
+    if (last_evals_per_iter >= 0 && last_evals_per_iter < kMinChainLeaves) return {1, 0u};
+    if (last_evals_per_iter >= 0 && last_evals_per_iter < mid_leaves)
+        return {std::max(1, std::min<int>(mid_chains, (int)(n / 64))), mid_grid};
+    return {std::max(1, std::min<int>(2, (int)(n / 64))), 0u};
 }
 
 // upload host root bookkeeping for trees [t0, t0+n)
@@ -447,7 +462,8 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
     if (n == 0) return SPAI_OK;
     hipStream_t st = e->stream;
     // chain h searches active[off[h] .. off[h] + cnt[h]) on chain_stream[h]
-    const int nchain = chains_for(n, e->last_evals_per_iter);
+    const ChainPolicy pol = chains_for(n, e->last_evals_per_iter);
+    const int nchain = pol.chains;
     uint32_t off[spai_engine::kChains] = {0, 0, 0, 0}, cnt[spai_engine::kChains] = {0, 0, 0, 0};
     for (int h = 0; h < nchain; ++h) {
         off[h] = (uint32_t)((uint64_t)n * h / nchain);
@@ -483,7 +499,8 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
             }
             if (sample) SPAI_TRY(timer_record(e, 1, it, true, sh, h));
             if (kind == SPAI_EVAL_NET) {
-                SPAI_TRY(net_eval_batch(e->net, sh, bv.count, nh, bv.mine, bv.theirs, bv.priors, bv.value));
+                SPAI_TRY(net_eval_batch(e->net, sh, bv.count, nh, bv.mine, bv.theirs, bv.priors, bv.value,
+                                        pol.grid_cap));
             } else {
                 k_eval_stub<<<(nh + kBlock - 1) / kBlock, kBlock, 0, sh>>>(bv, nh, kind);
             }

@@ -205,7 +205,7 @@ int net_bench(spai_net *net, uint32_t n, uint32_t iters, double *ms);
 void net_init_params(int game, int blocks, int hidden, uint64_t seed, float *params);
 // evaluate `count` (device scalar) leaves of the batch; grid sized for max_n
 int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint32_t max_n,
-                   const uint64_t *mine, const uint64_t *theirs, float *priors, float *value);
+                   const uint64_t *mine, const uint64_t *theirs, float *priors, float *value, uint32_t grid_cap = 0);
 
 // net_c4_f32.hip
 int net_create_f32(spai_net *n, const float *params);
