@@ -105,28 +105,36 @@ __device__ __forceinline__ void stage_planes(const float *__restrict__ xb, int c
     }
 }
 
-// Wk[(tap * cinp + c) * coutp + n]: forward Wk = w[n][c][tap]; data gradient Wk = w[c][n][8 - tap]
-__global__ void k_pack_wk(const float *__restrict__ w, int cin, int cout, int cinp, int coutp, int dgrad,
-                          float *__restrict__ wk) {
+// Wk[(tap * cinp + c) * coutp + n]: forward Wk = w[n][c][tap]; data gradient Wk = w[c][n][8 - tap].
+// Every conv's forward and data-gradient matrices are packed in one launch per
+// step (blockIdx.y = entry of the table built at learner_create):
+//   desc[8 y ..] = {param offset, cin, cout, cinp, coutp, dgrad, packed offset, 0}
+constexpr int kPackDesc = 8;
+__global__ void k_pack_all(const float *__restrict__ P, const uint32_t *__restrict__ desc, float *__restrict__ wall) {
+    const uint32_t *d = desc + kPackDesc * blockIdx.y;
+    const int cin = (int)d[1], cout = (int)d[2], cinp = (int)d[3], coutp = (int)d[4];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= 9 * cinp * coutp) return;
+    const float *w = P + d[0];
     const int n = i % coutp, k = i / coutp, tap = k / cinp, c = k - tap * cinp;
     float v = 0.f;
     if (c < cin && n < cout)
-        v = dgrad ? w[((size_t)c * cout + n) * 9 + (8 - tap)] : w[((size_t)n * cin + c) * 9 + tap];
-    wk[i] = v;
+        v = d[5] ? w[((size_t)c * cout + n) * 9 + (8 - tap)] : w[((size_t)n * cin + c) * 9 + tap];
+    wall[d[6] + i] = v;
 }
 
-// one workgroup per sample: 3 position tiles (48 rows, 42 real) x NT = coutp/16
-// channel tiles; wave w owns channel tile w % NT and K part w / NT (KS = 4/NT
-// parts, summed in LDS in a fixed order).  CINP (input channels padded to 4) and
-// NT are compile-time, so the k-loop unrolls fully and the weight loads of a
-// whole part are in flight together.
-template <int CINP, int NT>
+// workgroup (sample, slice): 3 position tiles (48 rows, 42 real) x NT channel
+// tiles of output channels [16 NT slice, 16 NT (slice + 1)); wave w owns channel
+// tile w % NT and K part w / NT (KS = 4/NT parts, summed in LDS in a fixed
+// order).  CINP (input channels padded to 4) and NT are compile-time, so the
+// k-loop unrolls fully and the weight loads of a whole part are in flight
+// together.  coutp_all = the packed matrix's row length (all output channels).
+template <int CINP, int NT, int MTS = 3>
 __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict__ in, int cin,
                                                         const float *__restrict__ wk, const float *__restrict__ bias,
-                                                        int cout, float *__restrict__ out, int accumulate) {
-    constexpr int KS = 4 / NT, COUTP = 16 * NT, CSN = CINP / 4, KSTEPS = 9 * CSN, PER = KSTEPS / KS;
+                                                        int cout, int coutp_all, float *__restrict__ out,
+                                                        int accumulate) {
+    constexpr int KS = 4 / NT, CSN = CINP / 4, KSTEPS = 9 * CSN, PER = KSTEPS / KS;
     static_assert(KSTEPS % KS == 0, "K parts must be whole k-steps");
     extern __shared__ float sm[];
     float *xs = sm;                          // [CINP][kPlane]
@@ -138,26 +146,32 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
     if (part >= KS) return;   // NT = 3 would leave a wave without a part (no barrier follows)
     const int s0 = part * PER;
     const int row = lane & 15, kq = lane >> 4;
-    int pbase[3];
-    bool pval[3];
+    // MTS = 3: the workgroup covers all 3 position tiles and blockIdx.y picks the
+    // channel slice; MTS = 1: blockIdx.y picks the position tile (all channels)
+    const int mt0 = MTS == 3 ? 0 : (int)blockIdx.y;
+    int pbase[MTS];
+    bool pval[MTS];
 #pragma unroll
-    for (int mt = 0; mt < 3; ++mt) {
-        const int p = mt * 16 + row;
+    for (int mt = 0; mt < MTS; ++mt) {
+        const int p = (mt0 + mt) * 16 + row;
         pval[mt] = p < kCells;
         const int pp = pval[mt] ? p : 0;
         pbase[mt] = (pp / kCols + 1) * 9 + pp % kCols + 1;
     }
-    f32x4 acc[3] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-    const float *wl = wk + (size_t)(4 * s0 + kq) * COUTP + nt * 16 + row;
+    f32x4 acc[MTS];
+#pragma unroll
+    for (int mt = 0; mt < MTS; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int co0 = MTS == 3 ? 16 * NT * (int)blockIdx.y : 0;
+    const float *wl = wk + (size_t)(4 * s0 + kq) * coutp_all + co0 + nt * 16 + row;
     float bq[PER];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) bq[i] = wl[(size_t)i * 4 * COUTP];
+    for (int i = 0; i < PER; ++i) bq[i] = wl[(size_t)i * 4 * coutp_all];
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
         const int s = s0 + i, tap = s / CSN, cs = s % CSN;   // CSN is a power of two here: shifts
         const float *xc = xs + (4 * cs + kq) * kPlane + tap_off(tap);
 #pragma unroll
-        for (int mt = 0; mt < 3; ++mt) {
+        for (int mt = 0; mt < MTS; ++mt) {
             const float av = pval[mt] ? xc[pbase[mt]] : 0.f;
             acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bq[i], acc[mt], 0, 0, 0);
         }
@@ -166,7 +180,7 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
         if (part > 0) {
             float *dst = red + (((part - 1) * 3) * 64 + lane) * 4 + nt * (3 * 3 * 64 * 4);
 #pragma unroll
-            for (int mt = 0; mt < 3; ++mt)
+            for (int mt = 0; mt < MTS; ++mt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) dst[mt * 64 * 4 + r] = acc[mt][r];
         }
@@ -176,20 +190,20 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
         for (int q = 1; q < KS; ++q) {
             const float *src = red + (((q - 1) * 3) * 64 + lane) * 4 + nt * (3 * 3 * 64 * 4);
 #pragma unroll
-            for (int mt = 0; mt < 3; ++mt)
+            for (int mt = 0; mt < MTS; ++mt)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) acc[mt][r] += src[mt * 64 * 4 + r];
         }
     }
-    const int n = nt * 16 + row;   // D[row = 4 kq + r][col = lane & 15]: col = channel, row = position
+    const int n = co0 + nt * 16 + row;   // D[row = 4 kq + r][col = lane & 15]: col = channel, row = position
     if (n >= cout) return;
     const float bn = bias ? bias[n] : 0.f;
     float *ob = out + ((size_t)b * cout + n) * kCells;
 #pragma unroll
-    for (int mt = 0; mt < 3; ++mt)
+    for (int mt = 0; mt < MTS; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int p = mt * 16 + 4 * kq + r;
+            const int p = (mt0 + mt) * 16 + 4 * kq + r;
             if (p < kCells) {
                 const float v = acc[mt][r] + bn;
                 ob[p] = accumulate ? ob[p] + v : v;
@@ -200,15 +214,18 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
 // weight-gradient partials: workgroup (chunk, group) accumulates, over the
 // kWgSamples samples of its chunk, the output tiles of its tile group:
 //   part[chunk][n][k] = sum_{b in chunk} sum_p dz[b][n][p] * X[b][p][k]   (k tap-major over CINP)
-//   partb[chunk][n]   = sum_{b in chunk} sum_p dz[b][n][p]
+// (the conv bias gradient, sum dz, comes out of the BN backward, k_bn_bwd)
 // GEMM rows = output channels (coutp/16 tiles), columns = k (round16(9 CINP)/16
 // tiles), reduction = each sample's 42 positions (11 k-steps of 4).
 constexpr int kWgSamples = 4;
-constexpr int kWgMaxTiles = 9;   // tiles per wave (144 tiles / 4 groups / 4 waves at 64 x 64)
+#ifndef SPAI_WG_TILES
+#define SPAI_WG_TILES 5
+#endif
+constexpr int kWgMaxTiles = SPAI_WG_TILES;   // tiles per wave (144 tiles / 8 groups / 4 waves at 64 x 64: 256 workgroups at B = 128)
 template <int CINP>
 __global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict__ x, int cin,
                                                          const float *__restrict__ dz, int cout, int B, int groups,
-                                                         float *__restrict__ part, float *__restrict__ partb) {
+                                                         float *__restrict__ part) {
     constexpr int K = 9 * CINP, Kp = (K + 15) & ~15, NK = Kp / 16;
     extern __shared__ float sm[];
     const int coutp = round16(cout), NTo = coutp / 16, ntiles = NTo * NK;
@@ -230,7 +247,6 @@ __global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict
     f32x4 acc[kWgMaxTiles];
 #pragma unroll
     for (int j = 0; j < kWgMaxTiles; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float accb = 0.f;
     const int b0 = chunk * kWgSamples, b1 = min(B, b0 + kWgSamples);
     // the next sample's planes and dz rows are loaded into registers while the
     // current sample's MFMAs run (one exposed round trip per chunk, not per sample)
@@ -244,11 +260,6 @@ __global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict
         if (b + 1 < b1) {
             load_planes(x + (size_t)(b + 1) * cin * kCells, cin, CINP, vx);
             load_dz(dz + (size_t)(b + 1) * cout * kCells, cout, coutp, vd);
-        }
-        if (group == 0 && threadIdx.x < cout) {   // bias partial (fixed order)
-            float t = 0.f;
-            for (int p = 0; p < kCells; ++p) t += ds[threadIdx.x * 44 + p];
-            accb += t;
         }
 #pragma unroll
         for (int j = 0; j < kWgMaxTiles; ++j) {
@@ -269,7 +280,6 @@ __global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict
         }
         __syncthreads();   // xs / ds are restaged for the next sample
     }
-    if (group == 0 && threadIdx.x < cout) partb[(size_t)chunk * cout + threadIdx.x] = accb;
 #pragma unroll
     for (int j = 0; j < kWgMaxTiles; ++j) {
         const int t = t0 + wave + 4 * j;
@@ -284,9 +294,8 @@ __global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict
     }
 }
 
-// dW[n][c][tap] = sum_chunk part[chunk][n][tap * cinp + c];  db[n] = sum_chunk partb[chunk][n]  (fixed order)
-__global__ void k_wgrad_reduce(const float *__restrict__ part, const float *__restrict__ partb, int B, int cin,
-                               int cout, float *__restrict__ dw, float *__restrict__ db) {
+// dW[n][c][tap] = sum_chunk part[chunk][n][tap * cinp + c]  (fixed order)
+__global__ void k_wgrad_reduce(const float *__restrict__ part, int B, int cin, int cout, float *__restrict__ dw) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int cinp = round4(cin), K = 9 * cinp;
     if (i < cout * K) {   // i = n * K + k: consecutive threads read consecutive partials (coalesced)
@@ -306,14 +315,141 @@ __global__ void k_wgrad_reduce(const float *__restrict__ part, const float *__re
             dw[((size_t)n * cin + c) * 9 + tap] = s;
         }
     }
-    if (i < cout) {
-        float s = 0.f;
-        for (int b = 0; b < B; ++b) s += partb[(size_t)b * cout + i];
-        db[i] = s;
-    }
 }
 
 // ------------------------------------------------------------------ batch norm
+// One workgroup of kBn threads per channel.  A channel's B x 42 values are read
+// once into registers (kBnPer per thread; batches past kBn * kBnPer = 6144
+// values, B > 146, re-read the rest from memory), so the two-pass statistics
+// and the output cost one memory pass.  Sums: fixed-order wave shuffles, then
+// the 16 wave partials in order (deterministic).
+constexpr int kBn = 1024, kBnPer = 6;
+__device__ __forceinline__ float bn_block_sum(float v, float *red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < kBn / 64; ++w) t += red[w];
+    return t;
+}
+__device__ __forceinline__ size_t bn_at(int i, int c, int c_n) {
+    return ((size_t)(i / kCells) * c_n + c) * kCells + i % kCells;
+}
+
+// forward in train mode, per channel: batch mean and biased variance over
+// (B, 42) (two passes over the registers), invstd = 1/sqrt(var + eps); running
+// stats r = (1 - m) r + m * stat (unbiased var); a = relu(gamma * (z - mean) *
+// invstd + beta [+ res])
+__global__ __launch_bounds__(kBn) void k_bn_fwd(const float *__restrict__ z, int c_n, int B, float eps,
+                                                float momentum, float *__restrict__ mean, float *__restrict__ invstd,
+                                                float *__restrict__ run_mean, float *__restrict__ run_var,
+                                                const float *__restrict__ gamma, const float *__restrict__ beta,
+                                                const float *__restrict__ res, float *__restrict__ a) {
+    __shared__ float red[2][kBn / 64];
+    const int c = blockIdx.x, n = B * kCells;
+    float v[kBnPer];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < kBnPer; ++j) {
+        const int i = threadIdx.x + j * kBn;
+        v[j] = i < n ? z[bn_at(i, c, c_n)] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < kBnPer; ++j) s += v[j];
+    for (int i = threadIdx.x + kBnPer * kBn; i < n; i += kBn) s += z[bn_at(i, c, c_n)];
+    const float mu = bn_block_sum(s, red[0]) / (float)n;
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < kBnPer; ++j)
+        if (threadIdx.x + j * kBn < n) q += (v[j] - mu) * (v[j] - mu);
+    for (int i = threadIdx.x + kBnPer * kBn; i < n; i += kBn) {
+        const float d = z[bn_at(i, c, c_n)] - mu;
+        q += d * d;
+    }
+    const float var = bn_block_sum(q, red[1]) / (float)n;
+    const float is = 1.0f / sqrtf(var + eps);
+    if (threadIdx.x == 0) {
+        mean[c] = mu;
+        invstd[c] = is;
+        run_mean[c] = (1.0f - momentum) * run_mean[c] + momentum * mu;
+        run_var[c] = (1.0f - momentum) * run_var[c] + momentum * (n > 1 ? var * (float)n / (float)(n - 1) : var);
+    }
+    const float ga = gamma[c], be = beta[c];
+    auto out = [&](int i, float zi) {
+        const size_t k = bn_at(i, c, c_n);
+        float y = ga * ((zi - mu) * is) + be;
+        if (res) y += res[k];
+        a[k] = fmaxf(y, 0.f);
+    };
+#pragma unroll
+    for (int j = 0; j < kBnPer; ++j)
+        if (threadIdx.x + j * kBn < n) out(threadIdx.x + j * kBn, v[j]);
+    for (int i = threadIdx.x + kBnPer * kBn; i < n; i += kBn) out(i, z[bn_at(i, c, c_n)]);
+}
+
+// backward of a = relu(bn(z) [+ res]): dy = da * (a > 0); per channel
+// dbeta = sum dy, dgamma = sum dy * xhat;  dz = gamma*invstd/N * (N dy - dbeta - xhat dgamma);
+// the conv bias gradient dbias = sum dz (zero up to rounding: the conv feeds the BN);
+// dy_out (optional) = dy, the residual block's skip-path gradient
+__global__ __launch_bounds__(kBn) void k_bn_bwd(const float *__restrict__ da, const float *__restrict__ a,
+                                                const float *__restrict__ z, int c_n, int B,
+                                                const float *__restrict__ mean, const float *__restrict__ invstd,
+                                                const float *__restrict__ gamma, float *__restrict__ dgamma,
+                                                float *__restrict__ dbeta, float *__restrict__ dbias,
+                                                float *__restrict__ dz, float *__restrict__ dy_out) {
+    __shared__ float red[3][kBn / 64];
+    const int c = blockIdx.x, n = B * kCells;
+    const float mu = mean[c], is = invstd[c];
+    float dy[kBnPer], xh[kBnPer];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < kBnPer; ++j) {
+        const int i = threadIdx.x + j * kBn;
+        const bool ok = i < n;
+        const size_t k = ok ? bn_at(i, c, c_n) : 0;
+        const float vd = ok ? da[k] : 0.f, va = ok ? a[k] : 0.f, vz = ok ? z[k] : mu;
+        dy[j] = va > 0.f ? vd : 0.f;
+        xh[j] = (vz - mu) * is;
+    }
+#pragma unroll
+    for (int j = 0; j < kBnPer; ++j) {
+        s1 += dy[j];
+        s2 += dy[j] * xh[j];
+    }
+    for (int i = threadIdx.x + kBnPer * kBn; i < n; i += kBn) {
+        const size_t k = bn_at(i, c, c_n);
+        const float d = a[k] > 0.f ? da[k] : 0.f;
+        s1 += d;
+        s2 += d * ((z[k] - mu) * is);
+    }
+    const float sb = bn_block_sum(s1, red[0]), sg = bn_block_sum(s2, red[1]);
+    const float g = gamma[c] * is / (float)n;
+    float s3 = 0.f;
+    auto out = [&](int i, float d, float x) {
+        const size_t k = bn_at(i, c, c_n);
+        const float v = g * ((float)n * d - sb - x * sg);
+        dz[k] = v;
+        if (dy_out) dy_out[k] = d;
+        s3 += v;
+    };
+#pragma unroll
+    for (int j = 0; j < kBnPer; ++j)
+        if (threadIdx.x + j * kBn < n) out(threadIdx.x + j * kBn, dy[j], xh[j]);
+    for (int i = threadIdx.x + kBnPer * kBn; i < n; i += kBn) {
+        const size_t k = bn_at(i, c, c_n);
+        out(i, a[k] > 0.f ? da[k] : 0.f, (z[k] - mu) * is);
+    }
+    const float sz = bn_block_sum(s3, red[2]);
+    if (threadIdx.x == 0) {
+        dbeta[c] = sb;
+        dgamma[c] = sg;
+        dbias[c] = sz;
+    }
+}
+
+// ------------------------------------------------------------------ heads + loss
 __device__ __forceinline__ float block_sum(float v, float *red) {
     red[threadIdx.x] = v;
     __syncthreads();
@@ -326,102 +462,6 @@ __device__ __forceinline__ float block_sum(float v, float *red) {
     return r;
 }
 
-// per channel: batch mean and biased variance over (B, 42) (two passes),
-// invstd = 1/sqrt(var + eps); running stats: r = (1 - m) r + m * stat (unbiased var)
-__global__ __launch_bounds__(kThreads) void k_bn_stats(const float *__restrict__ z, int c_n, int B, float eps,
-                                                       float momentum, float *__restrict__ mean,
-                                                       float *__restrict__ invstd, float *__restrict__ run_mean,
-                                                       float *__restrict__ run_var) {
-    __shared__ float red[kThreads];
-    const int c = blockIdx.x, n = B * kCells;
-    auto at = [&](int i) { return ((size_t)(i / kCells) * c_n + c) * kCells + i % kCells; };
-    float s = 0.f;
-    for (int i0 = threadIdx.x; i0 < n; i0 += 16 * kThreads) {   // 16 loads in flight, summed in order
-        float v[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = i0 + j * kThreads < n ? z[at(i0 + j * kThreads)] : 0.f;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) s += v[j];
-    }
-    const float mu = block_sum(s, red) / (float)n;
-    float q = 0.f;
-    for (int i0 = threadIdx.x; i0 < n; i0 += 16 * kThreads) {
-        float v[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) v[j] = i0 + j * kThreads < n ? z[at(i0 + j * kThreads)] - mu : 0.f;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) q += v[j] * v[j];
-    }
-    const float var = block_sum(q, red) / (float)n;
-    if (threadIdx.x == 0) {
-        mean[c] = mu;
-        invstd[c] = 1.0f / sqrtf(var + eps);
-        run_mean[c] = (1.0f - momentum) * run_mean[c] + momentum * mu;
-        run_var[c] = (1.0f - momentum) * run_var[c] + momentum * (n > 1 ? var * (float)n / (float)(n - 1) : var);
-    }
-}
-
-// a = relu(gamma * (z - mean) * invstd + beta [+ res])
-__global__ void k_bn_act(const float *__restrict__ z, int c_n, int B, const float *__restrict__ mean,
-                         const float *__restrict__ invstd, const float *__restrict__ gamma,
-                         const float *__restrict__ beta, const float *__restrict__ res, float *__restrict__ a) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (size_t)B * c_n * kCells) return;
-    const int c = (int)((i / kCells) % c_n);
-    float y = gamma[c] * ((z[i] - mean[c]) * invstd[c]) + beta[c];
-    if (res) y += res[i];
-    a[i] = fmaxf(y, 0.f);
-}
-
-// backward of a = relu(bn(z) [+ res]): dy = da * (a > 0); per channel
-// dbeta = sum dy, dgamma = sum dy * xhat;  dz = gamma*invstd/N * (N dy - dbeta - xhat dgamma)
-__global__ __launch_bounds__(kThreads) void k_bn_bwd(const float *__restrict__ da, const float *__restrict__ a,
-                                                     const float *__restrict__ z, int c_n, int B,
-                                                     const float *__restrict__ mean, const float *__restrict__ invstd,
-                                                     const float *__restrict__ gamma, float *__restrict__ dgamma,
-                                                     float *__restrict__ dbeta, float *__restrict__ dz) {
-    __shared__ float red[kThreads];
-    const int c = blockIdx.x, n = B * kCells;
-    const float mu = mean[c], is = invstd[c];
-    auto at = [&](int i) { return ((size_t)(i / kCells) * c_n + c) * kCells + i % kCells; };
-    float s1 = 0.f, s2 = 0.f;
-    for (int i0 = threadIdx.x; i0 < n; i0 += 8 * kThreads) {   // 8 x 3 loads in flight, summed in order
-        float vd[8], va[8], vz[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const bool ok = i0 + j * kThreads < n;
-            const size_t k = ok ? at(i0 + j * kThreads) : 0;
-            vd[j] = ok ? da[k] : 0.f;
-            va[j] = ok ? a[k] : 0.f;
-            vz[j] = ok ? z[k] : mu;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float dy = va[j] > 0.f ? vd[j] : 0.f;
-            s1 += dy;
-            s2 += dy * ((vz[j] - mu) * is);
-        }
-    }
-    const float sb = block_sum(s1, red), sg = block_sum(s2, red);
-    if (threadIdx.x == 0) {
-        dbeta[c] = sb;
-        dgamma[c] = sg;
-    }
-    const float g = gamma[c] * is / (float)n;
-    for (int i = threadIdx.x; i < n; i += kThreads) {
-        const size_t k = ((size_t)(i / kCells) * c_n + c) * kCells + i % kCells;
-        const float dy = a[k] > 0.f ? da[k] : 0.f;
-        dz[k] = g * ((float)n * dy - sb - ((z[k] - mu) * is) * sg);
-    }
-}
-
-// dt = da * (a > 0) (the residual block's skip-path gradient)
-__global__ void k_relu_mask(const float *__restrict__ da, const float *__restrict__ a, size_t n, float *__restrict__ dt) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) dt[i] = a[i] > 0.f ? da[i] : 0.f;
-}
-
-// ------------------------------------------------------------------ heads + loss
 // one workgroup per sample: policy logits (1344 -> 7), value (126 -> 1, tanh),
 // loss terms and the output gradients
 //   dlogits = (softmax * sum(pi) - pi) / B,  dpre = 2 (v - z) / B * (1 - v^2)
@@ -561,67 +601,69 @@ int learner_alloc_batch(spai_learner *L, uint32_t B) {
     SPAI_TRY(L->loss_terms.alloc((size_t)B * 2));
     const size_t cmax = (size_t)std::max(L->hidden, 32);
     SPAI_TRY(L->wpart.alloc((size_t)B * cmax * 9 * round4(L->hidden)));   // per-sample weight-gradient partials
-    SPAI_TRY(L->bpart.alloc((size_t)B * cmax));
     L->max_batch = B;
     return SPAI_OK;
 }
 
-// out (+)= conv(in) on f32 MFMA; dgrad: flipped/transposed weights, no bias.
-// The learner's shapes: input channels 3 (-> 4), 32 or 64; output 3 (1 tile), 32 (2) or 64 (4).
+// out (+)= conv(in) on f32 MFMA with a packed weight matrix wk (forward or
+// data-gradient orientation, k_pack_all).  The learner's shapes: input channels
+// 3 (-> 4), 32 or 64; output 3 (1 tile), 32 (2) or 64 (4).  Where the k-steps
+// split into 4 whole parts (32 and 64 input channels) every 16-channel tile is
+// its own workgroup with the K split over its 4 waves (grid B x coutp/16: 4x
+// the workgroups of one per sample); the stem's input (4 padded channels, 9
+// k-steps) keeps one workgroup per sample with a wave per channel tile.
 template <int CINP>
-int launch_conv_t(int nt, dim3 grid, size_t lds, hipStream_t st, const float *in, int cin, const float *wk,
-                  const float *bias, int cout, float *out, int acc) {
-    constexpr int ks = 9 * CINP / 4;   // k-steps; a K split into 4/NT parts needs whole k-steps per part
-    if constexpr (ks % 4 == 0) {
-        if (nt == 1) {
-            k_conv_mfma<CINP, 1><<<grid, kThreads, lds, st>>>(in, cin, wk, bias, cout, out, acc);
-            return SPAI_OK;
-        }
+int launch_conv_t(int B, size_t lds, hipStream_t st, const float *in, int cin, const float *wk, const float *bias,
+                  int cout, float *out, int acc) {
+    constexpr int ks = 9 * CINP / 4;
+    const int nt = round16(cout) / 16;
+#ifdef SPAI_CONV_ROWS
+    if (nt == 4 && CINP >= 32) {   // one workgroup per (sample, position tile): the unsplit K order
+        k_conv_mfma<CINP, 4, 1><<<dim3(B, 3), kThreads, lds, st>>>(in, cin, wk, bias, cout, 64, out, acc);
+        return SPAI_OK;
     }
-    if constexpr (ks % 2 == 0) {
-        if (nt == 2) {
-            k_conv_mfma<CINP, 2><<<grid, kThreads, lds, st>>>(in, cin, wk, bias, cout, out, acc);
-            return SPAI_OK;
-        }
+#endif
+#ifndef SPAI_SLICE_MIN_CINP
+#define SPAI_SLICE_MIN_CINP 32
+#endif
+    if constexpr (ks % 4 == 0 && CINP >= SPAI_SLICE_MIN_CINP) {
+        k_conv_mfma<CINP, 1><<<dim3(B, nt), kThreads, lds, st>>>(in, cin, wk, bias, cout, 16 * nt, out, acc);
+        return SPAI_OK;
     }
     if (nt == 4) {
-        k_conv_mfma<CINP, 4><<<grid, kThreads, lds, st>>>(in, cin, wk, bias, cout, out, acc);
+        k_conv_mfma<CINP, 4><<<dim3(B), kThreads, lds, st>>>(in, cin, wk, bias, cout, 64, out, acc);
         return SPAI_OK;
     }
     set_error("learner conv: %d input / %d output channels not built", cin, cout);
     return SPAI_ERR_UNSUPPORTED;
 }
 
-int launch_conv(spai_learner *L, const float *in, int cin, const float *w, const float *bias, int cout, float *out,
-                int B, bool acc, bool dgrad, hipStream_t st) {
-    const int cinp = round4(cin), coutp = round16(cout);
-    k_pack_wk<<<blocks_of((size_t)9 * cinp * coutp), kThreads, 0, st>>>(w, cin, cout, cinp, coutp, dgrad ? 1 : 0,
-                                                                        L->wt.p);
+int launch_conv(const float *in, int cin, const float *wk, const float *bias, int cout, float *out, int B, bool acc,
+                hipStream_t st) {
+    const int cinp = round4(cin);
     const size_t lds = ((size_t)cinp * kPlane + 2 * 2304) * sizeof(float);
-    const int nt = coutp / 16, a = acc ? 1 : 0;
+    const int a = acc ? 1 : 0;
     switch (cinp) {
-    case 4: return launch_conv_t<4>(nt, dim3(B), lds, st, in, cin, L->wt.p, bias, cout, out, a);
-    case 32: return launch_conv_t<32>(nt, dim3(B), lds, st, in, cin, L->wt.p, bias, cout, out, a);
-    case 64: return launch_conv_t<64>(nt, dim3(B), lds, st, in, cin, L->wt.p, bias, cout, out, a);
+    case 4: return launch_conv_t<4>(B, lds, st, in, cin, wk, bias, cout, out, a);
+    case 32: return launch_conv_t<32>(B, lds, st, in, cin, wk, bias, cout, out, a);
+    case 64: return launch_conv_t<64>(B, lds, st, in, cin, wk, bias, cout, out, a);
     default: set_error("learner conv: %d input channels not built", cin); return SPAI_ERR_UNSUPPORTED;
     }
 }
 
 // dW, db of one conv: chunk partials on f32 MFMA, then a fixed-order sum over the chunks
-int launch_wgrad(spai_learner *L, const float *x, int cin, const float *dz, int cout, int B, float *dw, float *db,
-                 hipStream_t st) {
+int launch_wgrad(spai_learner *L, const float *x, int cin, const float *dz, int cout, int B, float *dw, hipStream_t st) {
     const int cinp = round4(cin), nk = (9 * cinp + 15) / 16, ntiles = (round16(cout) / 16) * nk;
     const int groups = std::max(1, (ntiles + 4 * kWgMaxTiles - 1) / (4 * kWgMaxTiles));
     const int chunks = (B + kWgSamples - 1) / kWgSamples;
     const size_t lds = ((size_t)cinp * kPlane + (size_t)round16(cout) * 44) * sizeof(float);
     const dim3 grid(chunks, groups);
     switch (cinp) {
-    case 4: k_wgrad_mfma<4><<<grid, kThreads, lds, st>>>(x, cin, dz, cout, B, groups, L->wpart.p, L->bpart.p); break;
-    case 64: k_wgrad_mfma<64><<<grid, kThreads, lds, st>>>(x, cin, dz, cout, B, groups, L->wpart.p, L->bpart.p); break;
+    case 4: k_wgrad_mfma<4><<<grid, kThreads, lds, st>>>(x, cin, dz, cout, B, groups, L->wpart.p); break;
+    case 64: k_wgrad_mfma<64><<<grid, kThreads, lds, st>>>(x, cin, dz, cout, B, groups, L->wpart.p); break;
     default: set_error("learner wgrad: %d input channels not built", cin); return SPAI_ERR_UNSUPPORTED;
     }
-    k_wgrad_reduce<<<blocks_of((size_t)cout * 9 * cinp), kThreads, 0, st>>>(L->wpart.p, L->bpart.p, chunks, cin, cout,
-                                                                           dw, db);
+    k_wgrad_reduce<<<blocks_of((size_t)cout * 9 * cinp), kThreads, 0, st>>>(L->wpart.p, chunks, cin, cout, dw);
     return SPAI_OK;
 }
 
@@ -642,7 +684,7 @@ int learner_create(spai_engine *e, int blocks, int hidden, const float *params, 
     else spai_adam_config_default(&L->cfg);
     size_t off = 0;
     auto conv = [&](int ci, int co) {
-        spai_learner::Conv c{ci, co, 0, 0, 0, 0, 0, 0};
+        spai_learner::Conv c{ci, co, 0, 0, 0, 0, 0, 0, 0, 0};
         c.w = off;
         off += (size_t)co * ci * 9;
         c.b = off;
@@ -676,7 +718,30 @@ int learner_create(spai_engine *e, int blocks, int hidden, const float *params, 
     chk(L->bsum.alloc(1));
     chk(L->m.alloc(n));
     chk(L->v.alloc(n));
-    chk(L->wt.alloc((size_t)9 * 64 * 64));   // packed [k][n] conv weights (cin, cout <= 64)
+    {   // packed [k][n] matrices: every conv forward, every conv but the stem data gradient
+        std::vector<uint32_t> desc;
+        size_t woff = 0;
+        auto entry = [&](size_t wparam, int cin, int cout, int dgrad) {
+            const int cinp = round4(cin), coutp = round16(cout);
+            desc.insert(desc.end(), {(uint32_t)wparam, (uint32_t)cin, (uint32_t)cout, (uint32_t)cinp, (uint32_t)coutp,
+                                     (uint32_t)dgrad, (uint32_t)woff, 0u});
+            woff += (size_t)9 * cinp * coutp;
+            return woff - (size_t)9 * cinp * coutp;
+        };
+        for (size_t l = 0; l < L->convs.size(); ++l) {
+            spai_learner::Conv &c = L->convs[l];
+            c.wk = entry(c.w, c.ci, c.co, 0);
+            c.wkd = l == 0 ? 0 : entry(c.w, c.co, c.ci, 1);
+        }
+        L->n_pack = (int)(desc.size() / kPackDesc);
+        chk(L->wt.alloc(woff));
+        chk(L->pack_desc.alloc(desc.size()));
+        if (rc == SPAI_OK &&
+            hipMemcpy(L->pack_desc.p, desc.data(), desc.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            set_error("learner: upload failed");
+            rc = SPAI_ERR_DEVICE;
+        }
+    }
     L->z.resize(L->convs.size());
     L->a.resize(L->convs.size());
     L->mean.resize(L->convs.size());
@@ -712,8 +777,9 @@ void learner_destroy(spai_learner *L) {
     if (!L) return;
     if (L->eng) (void)hipStreamSynchronize(L->eng->stream);
     if (L->comm) (void)ncclCommDestroy((ncclComm_t)L->comm);
+    L->pack_desc.release();
     for (auto *b : {&L->p, &L->g, &L->bsum, &L->m, &L->v, &L->wt, &L->x_in, &L->pi, &L->zv, &L->d0, &L->d1, &L->d2, &L->dlogits,
-                    &L->dpre, &L->loss_terms, &L->wpart, &L->bpart, &L->run_buf})
+                    &L->dpre, &L->loss_terms, &L->wpart, &L->run_buf})
         b->release();
     L->run_idx.release();
     for (auto *vec : {&L->z, &L->a, &L->mean, &L->invstd})
@@ -726,7 +792,6 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
     SPAI_CHECK(B >= 1, SPAI_ERR_INVALID, "train_batch: empty batch");
     SPAI_TRY(learner_alloc_batch(L, B));
     hipStream_t st = L->eng->stream;
-    const int H = L->hidden;
     float *P = L->p.p, *G = L->g.p;
     SPAI_HIP(hipMemcpyAsync(L->x_in.p, states, (size_t)B * 3 * kCells * 4, hipMemcpyHostToDevice, st));
     SPAI_HIP(hipMemcpyAsync(L->pi.p, policies, (size_t)B * 7 * 4, hipMemcpyHostToDevice, st));
@@ -734,18 +799,17 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
     SPAI_HIP(hipMemsetAsync(G, 0, L->n_params * 4, st));
     const float eps = L->cfg.bn_eps, mom = L->cfg.bn_momentum;
     const size_t nl = L->convs.size();
+    k_pack_all<<<dim3(blocks_of((size_t)9 * 64 * 64), L->n_pack), kThreads, 0, st>>>(P, L->pack_desc.p, L->wt.p);
+    const float *W = L->wt.p;
     const int pol = (int)nl - 2, val = (int)nl - 1;
 
     // ---------------- forward (train mode)
     int crc = SPAI_OK;   // conv launch status (shape dispatch)
     auto conv_bn_act = [&](int l, const float *in, const float *res) {
         const spai_learner::Conv &c = L->convs[l];
-        if (crc == SPAI_OK) crc = launch_conv(L, in, c.ci, P + c.w, P + c.b, c.co, L->z[l].p, (int)B, false, false, st);
-        k_bn_stats<<<c.co, kThreads, 0, st>>>(L->z[l].p, c.co, (int)B, eps, mom, L->mean[l].p, L->invstd[l].p, P + c.mu,
-                                              P + c.var);
-        k_bn_act<<<blocks_of((size_t)B * c.co * kCells), kThreads, 0, st>>>(L->z[l].p, c.co, (int)B, L->mean[l].p,
-                                                                          L->invstd[l].p, P + c.g, P + c.be, res,
-                                                                          L->a[l].p);
+        if (crc == SPAI_OK) crc = launch_conv(in, c.ci, W + c.wk, P + c.b, c.co, L->z[l].p, (int)B, false, st);
+        k_bn_fwd<<<c.co, kBn, 0, st>>>(L->z[l].p, c.co, (int)B, eps, mom, L->mean[l].p, L->invstd[l].p, P + c.mu,
+                                       P + c.var, P + c.g, P + c.be, res, L->a[l].p);
     };
     conv_bn_act(0, L->x_in.p, nullptr);
     const float *h = L->a[0].p;
@@ -761,7 +825,6 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
                                          L->loss_terms.p);
 
     // ---------------- backward
-    const size_t nact = (size_t)B * H * kCells;
     // heads: linears -> relu/BN -> conv; dh (d0) = dgrad(policy) + dgrad(value)
     k_linear_bwd_w<<<blocks_of(7 * 32 * kCells), kThreads, 0, st>>>(L->a[pol].p, L->dlogits.p, (int)B, 7, 32 * kCells,
                                                                      G + L->pol_w, G + L->pol_b);
@@ -769,10 +832,10 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
                                                                              32 * kCells, L->d1.p);
     auto bn_conv_bwd = [&](int l, const float *da, const float *in, float *dx, bool acc) {
         const spai_learner::Conv &c = L->convs[l];
-        k_bn_bwd<<<c.co, kThreads, 0, st>>>(da, L->a[l].p, L->z[l].p, c.co, (int)B, L->mean[l].p, L->invstd[l].p,
-                                            P + c.g, G + c.g, G + c.be, L->d2.p);
-        if (crc == SPAI_OK) crc = launch_wgrad(L, in, c.ci, L->d2.p, c.co, (int)B, G + c.w, G + c.b, st);
-        if (dx && crc == SPAI_OK) crc = launch_conv(L, L->d2.p, c.co, P + c.w, nullptr, c.ci, dx, (int)B, acc, true, st);
+        k_bn_bwd<<<c.co, kBn, 0, st>>>(da, L->a[l].p, L->z[l].p, c.co, (int)B, L->mean[l].p, L->invstd[l].p,
+                                       P + c.g, G + c.g, G + c.be, G + c.b, L->d2.p, nullptr);
+        if (crc == SPAI_OK) crc = launch_wgrad(L, in, c.ci, L->d2.p, c.co, (int)B, G + c.w, st);
+        if (dx && crc == SPAI_OK) crc = launch_conv(L->d2.p, c.co, W + c.wkd, nullptr, c.ci, dx, (int)B, acc, st);
     };
     bn_conv_bwd(pol, L->d1.p, h, L->d0.p, false);
     k_linear_bwd_w<<<blocks_of(3 * kCells), kThreads, 0, st>>>(L->a[val].p, L->dpre.p, (int)B, 1, 3 * kCells,
@@ -784,16 +847,15 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
     for (int k = L->blocks - 1; k >= 0; --k) {
         const int l1 = 1 + 2 * k, l2 = 2 + 2 * k;
         const float *hin = k == 0 ? L->a[0].p : L->a[l2 - 2].p;
-        // dt = d(out) * (out > 0): gradient of the pre-ReLU sum, shared by the skip path and BN2
-        k_relu_mask<<<blocks_of(nact), kThreads, 0, st>>>(L->d0.p, L->a[l2].p, nact, L->d1.p);
-        // BN2/conv2 backward on dy2 = dt (the mask a[l2] > 0 inside k_bn_bwd is idempotent on dt);
-        // conv2's input is a[l1]; its data gradient overwrites d0 with dL/d(relu1 output)
+        // BN2/conv2 backward: dt = d(out) * (out > 0) is the gradient of the pre-ReLU sum, shared
+        // by BN2 and the skip path (k_bn_bwd also writes it to d1); conv2's input is a[l1]; its
+        // data gradient overwrites d0 with dL/d(relu1 output)
         {
             const spai_learner::Conv &c = L->convs[l2];
-            k_bn_bwd<<<c.co, kThreads, 0, st>>>(L->d1.p, L->a[l2].p, L->z[l2].p, c.co, (int)B, L->mean[l2].p,
-                                                L->invstd[l2].p, P + c.g, G + c.g, G + c.be, L->d2.p);
-            if (crc == SPAI_OK) crc = launch_wgrad(L, L->a[l1].p, c.ci, L->d2.p, c.co, (int)B, G + c.w, G + c.b, st);
-            if (crc == SPAI_OK) crc = launch_conv(L, L->d2.p, c.co, P + c.w, nullptr, c.ci, L->d0.p, (int)B, false, true, st);
+            k_bn_bwd<<<c.co, kBn, 0, st>>>(L->d0.p, L->a[l2].p, L->z[l2].p, c.co, (int)B, L->mean[l2].p,
+                                           L->invstd[l2].p, P + c.g, G + c.g, G + c.be, G + c.b, L->d2.p, L->d1.p);
+            if (crc == SPAI_OK) crc = launch_wgrad(L, L->a[l1].p, c.ci, L->d2.p, c.co, (int)B, G + c.w, st);
+            if (crc == SPAI_OK) crc = launch_conv(L->d2.p, c.co, W + c.wkd, nullptr, c.ci, L->d0.p, (int)B, false, st);
         }
         // BN1/conv1 backward: da = d0 (gradient wrt relu1 output), mask a[l1]; its input is hin;
         // dgrad accumulates into d1 (= dt, the skip gradient) -> d(block input)

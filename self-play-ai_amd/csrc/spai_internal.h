@@ -140,16 +140,19 @@ struct spai_learner {
     struct Conv {
         int ci, co;
         size_t w, b, g, be, mu, var;   // offsets into the flat parameter array
+        size_t wk, wkd;                // offsets of its packed forward / data-gradient matrices in wt
     };
     std::vector<Conv> convs;            // stem, 2*blocks residual, policy head, value head
     size_t pol_w = 0, pol_b = 0, val_w = 0, val_b = 0;
     spai::DevBuf<float> p, g, m, v;     // params, grads, Adam moments (flat)
     spai::DevBuf<float> bsum;           // data parallel: sum over ranks of the batch size
-    spai::DevBuf<float> wt;             // flipped/transposed conv weights for the data gradient
+    spai::DevBuf<float> wt;             // packed conv matrices (forward and data gradient), once per step
+    spai::DevBuf<uint32_t> pack_desc;   // their table (k_pack_all)
+    int n_pack = 0;
     spai::DevBuf<float> x_in, pi, zv;   // batch
     std::vector<spai::DevBuf<float>> z, a, mean, invstd;   // per conv layer
     spai::DevBuf<float> d0, d1, d2;     // backward scratch [B][64][42]
-    spai::DevBuf<float> dlogits, dpre, loss_terms, wpart, bpart;
+    spai::DevBuf<float> dlogits, dpre, loss_terms, wpart;
     spai::DevBuf<uint32_t> run_idx;     // BN running-stat offsets (for the cross-rank average)
     spai::DevBuf<float> run_buf;
     void *comm = nullptr;            // ncclComm_t (learner.hip)

@@ -470,7 +470,21 @@ def test_learner_vs_torch_golden(spai):
     e.close()
 
 
-@pytest.mark.parametrize("blocks,B,steps", [(2, 48, 2), (6, 128, 1), (0, 5, 1)])
+def _check_grads_kinks(g, ref):
+    """fp32 gradient vs the float64 restatement.  Bulk: 3e-4 * max|g| (fp32 through
+    2*blocks+3 layers).  A pre-ReLU value within fp32 rounding of 0 (BN beta is 0 at
+    init, so y = gamma * xhat crosses 0 inside the batch) takes either side of the
+    kink depending on the summation order, and the float64 answer itself jumps by
+    ~5e-4 * max|g| under a 1-ulp parameter perturbation (scripts/learner_conditioning.py:
+    6 blocks / batch 128 gives 4.9e-4, 4.9e-4, 3e-7 for three perturbations).  Such a
+    flip moves the gradients of one channel's weights, so at most 1 % of the entries
+    may leave the bulk bound, and none may exceed 3e-3 * max|g|."""
+    d, m = np.abs(g - ref), np.abs(ref).max()
+    assert d.max() <= 3e-3 * m, d.max() / m
+    assert np.mean(d > 3e-4 * m) <= 0.01, np.mean(d > 3e-4 * m)
+
+
+@pytest.mark.parametrize("blocks,B,steps", [(2, 48, 2), (6, 128, 1), (2, 128, 1), (0, 5, 1)])
 def test_learner_vs_oracle(spai, oracle, blocks, B, steps):
     """other depths and batch sizes (incl. the reference's 128 and a tiny odd one)
     vs the numpy float64 restatement"""
@@ -496,7 +510,7 @@ def test_learner_vs_oracle(spai, oracle, blocks, B, steps):
     P_ref, ref_losses, ref_grads = LR.train(p0, batches, blocks, 64)
     np.testing.assert_allclose(dev_losses[0], ref_losses[0], rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(np.array(dev_losses), ref_losses, rtol=1e-3, atol=1e-4)
-    assert np.abs(g1 - ref_grads[0]).max() <= 3e-4 * np.abs(ref_grads[0]).max()   # fp32 through 2*blocks+3 layers
+    _check_grads_kinks(g1, ref_grads[0])
     check_learner_params(L.params(), P_ref, ref_grads, blocks, 64, steps, tol=1e-4)
     L.close()
     e.close()
