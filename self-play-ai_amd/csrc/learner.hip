@@ -135,17 +135,22 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
                                                         int cout, int coutp_all, float *__restrict__ out,
                                                         int accumulate) {
     constexpr int KS = 4 / NT, CSN = CINP / 4, KSTEPS = 9 * CSN, PER = KSTEPS / KS;
-    static_assert(KSTEPS % KS == 0, "K parts must be whole k-steps");
+    static_assert(4 % NT == 0 && KSTEPS % KS == 0, "4 waves: NT channel tiles x KS whole K parts");
     extern __shared__ float sm[];
     float *xs = sm;                          // [CINP][kPlane]
     float *red = sm + CINP * kPlane;         // K-split partials [3 parts][3 mt][64 lanes][4] per channel tile
     const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    stage_planes(in + (size_t)b * cin * kCells, cin, CINP, xs);
-    __syncthreads();
     const int nt = wave % NT, part = wave / NT;
-    if (part >= KS) return;   // NT = 3 would leave a wave without a part (no barrier follows)
     const int s0 = part * PER;
     const int row = lane & 15, kq = lane >> 4;
+    // this wave's weights first: their loads are in flight while the planes stage
+    const int co0 = MTS == 3 ? 16 * NT * (int)blockIdx.y : 0;
+    const float *wl = wk + (size_t)(4 * s0 + kq) * coutp_all + co0 + nt * 16 + row;
+    float bq[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) bq[i] = wl[(size_t)i * 4 * coutp_all];
+    stage_planes(in + (size_t)b * cin * kCells, cin, CINP, xs);
+    __syncthreads();
     // MTS = 3: the workgroup covers all 3 position tiles and blockIdx.y picks the
     // channel slice; MTS = 1: blockIdx.y picks the position tile (all channels)
     const int mt0 = MTS == 3 ? 0 : (int)blockIdx.y;
@@ -161,11 +166,6 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
     f32x4 acc[MTS];
 #pragma unroll
     for (int mt = 0; mt < MTS; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int co0 = MTS == 3 ? 16 * NT * (int)blockIdx.y : 0;
-    const float *wl = wk + (size_t)(4 * s0 + kq) * coutp_all + co0 + nt * 16 + row;
-    float bq[PER];
-#pragma unroll
-    for (int i = 0; i < PER; ++i) bq[i] = wl[(size_t)i * 4 * coutp_all];
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
         const int s = s0 + i, tap = s / CSN, cs = s % CSN;   // CSN is a power of two here: shifts
@@ -217,11 +217,14 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
 // (the conv bias gradient, sum dz, comes out of the BN backward, k_bn_bwd)
 // GEMM rows = output channels (coutp/16 tiles), columns = k (round16(9 CINP)/16
 // tiles), reduction = each sample's 42 positions (11 k-steps of 4).
-constexpr int kWgSamples = 4;
-#ifndef SPAI_WG_TILES
-#define SPAI_WG_TILES 5
+#ifndef SPAI_WG_SAMPLES
+#define SPAI_WG_SAMPLES 4
 #endif
-constexpr int kWgMaxTiles = SPAI_WG_TILES;   // tiles per wave (144 tiles / 8 groups / 4 waves at 64 x 64: 256 workgroups at B = 128)
+constexpr int kWgSamples = SPAI_WG_SAMPLES;
+#ifndef SPAI_WG_TILES
+#define SPAI_WG_TILES 3
+#endif
+constexpr int kWgMaxTiles = SPAI_WG_TILES;   // tiles per wave (144 tiles / 12 groups / 4 waves at 64 x 64: 384 workgroups at B = 128)
 template <int CINP>
 __global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict__ x, int cin,
                                                          const float *__restrict__ dz, int cout, int B, int groups,
@@ -392,13 +395,14 @@ __global__ __launch_bounds__(kBn) void k_bn_fwd(const float *__restrict__ z, int
 // backward of a = relu(bn(z) [+ res]): dy = da * (a > 0); per channel
 // dbeta = sum dy, dgamma = sum dy * xhat;  dz = gamma*invstd/N * (N dy - dbeta - xhat dgamma);
 // the conv bias gradient dbias = sum dz (zero up to rounding: the conv feeds the BN);
-// dy_out (optional) = dy, the residual block's skip-path gradient
+// dy_out (optional) = dy, the residual block's skip-path gradient.  dz may be z
+// itself (every element is read and written by the same thread)
 __global__ __launch_bounds__(kBn) void k_bn_bwd(const float *__restrict__ da, const float *__restrict__ a,
-                                                const float *__restrict__ z, int c_n, int B,
+                                                const float *z, int c_n, int B,
                                                 const float *__restrict__ mean, const float *__restrict__ invstd,
                                                 const float *__restrict__ gamma, float *__restrict__ dgamma,
-                                                float *__restrict__ dbeta, float *__restrict__ dbias,
-                                                float *__restrict__ dz, float *__restrict__ dy_out) {
+                                                float *__restrict__ dbeta, float *__restrict__ dbias, float *dz,
+                                                float *__restrict__ dy_out) {
     __shared__ float red[3][kBn / 64];
     const int c = blockIdx.x, n = B * kCells;
     const float mu = mean[c], is = invstd[c];
@@ -504,29 +508,37 @@ __global__ __launch_bounds__(kThreads) void k_heads_loss(const float *__restrict
 
 // linear backward, out features O, in features K:
 //   dW[o][k] = sum_b dy[b][o] x[b][k];  db[o] = sum_b dy[b][o];  dx[b][k] = sum_o dy[b][o] W[o][k]
-__global__ void k_linear_bwd_w(const float *__restrict__ x, const float *__restrict__ dy, int B, int O, int K,
-                               float *__restrict__ dw, float *__restrict__ db) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// dw[o][k] = sum_b dy[b][o] x[b][k], db[o] = sum_b dy[b][o].  A workgroup owns 64
+// outputs; its 4 waves take a quarter of the batch each (16 loads in flight),
+// and the quarters are added in order through LDS.
+__global__ __launch_bounds__(kThreads) void k_linear_bwd_w(const float *__restrict__ x, const float *__restrict__ dy,
+                                                           int B, int O, int K, float *__restrict__ dw,
+                                                           float *__restrict__ db) {
+    __shared__ float part[4][64];
+    const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+    const int i = blockIdx.x * 64 + lane;
+    const int bq0 = B * q / 4, bq1 = B * (q + 1) / 4;
+    float s = 0.f;
     if (i < O * K) {
         const int o = i / K, k = i - o * K;
-        float s = 0.f;
-        for (int b0 = 0; b0 < B; b0 += 16) {   // 16 loads in flight, summed in batch order
+        for (int b0 = bq0; b0 < bq1; b0 += 16) {
             float v[16];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) v[j] = b0 + j < B ? x[(size_t)(b0 + j) * K + k] : 0.f;
+            for (int j = 0; j < 16; ++j) v[j] = b0 + j < bq1 ? x[(size_t)(b0 + j) * K + k] : 0.f;
 #pragma unroll
             for (int j = 0; j < 16; ++j)
-                if (b0 + j < B) s += dy[(b0 + j) * O + o] * v[j];
+                if (b0 + j < bq1) s += dy[(b0 + j) * O + o] * v[j];
         }
-        dw[i] = s;
     }
-    if (i < O) {
-        float s = 0.f;
-        for (int b = 0; b < B; ++b) s += dy[b * O + i];
-        db[i] = s;
+    part[q][lane] = s;
+    __syncthreads();
+    if (q == 0 && i < O * K) dw[i] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+    if (blockIdx.x == 0 && q == 1 && lane < O) {
+        float t = 0.f;
+        for (int b = 0; b < B; ++b) t += dy[b * O + lane];
+        db[lane] = t;
     }
 }
-
 __global__ void k_linear_bwd_x(const float *__restrict__ dy, const float *__restrict__ w, int B, int O, int K,
                                float *__restrict__ dx) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -595,7 +607,6 @@ int learner_alloc_batch(spai_learner *L, uint32_t B) {
     }
     SPAI_TRY(L->d0.alloc(act));
     SPAI_TRY(L->d1.alloc(act));
-    SPAI_TRY(L->d2.alloc(act));
     SPAI_TRY(L->dlogits.alloc((size_t)B * 7));
     SPAI_TRY(L->dpre.alloc(B));
     SPAI_TRY(L->loss_terms.alloc((size_t)B * 2));
@@ -754,6 +765,17 @@ int learner_create(spai_engine *e, int blocks, int hidden, const float *params, 
         for (int c = 0; c < L->convs[l].co; ++c) ridx.push_back((uint32_t)(L->convs[l].var + c));
     }
     chk(L->run_idx.alloc(ridx.size()));
+    L->ev_dz.assign(L->convs.size(), nullptr);
+    if (hipStreamCreateWithFlags(&L->wg_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&L->ev_wg_done, hipEventDisableTiming) != hipSuccess) {
+        set_error("learner: stream/event creation failed");
+        rc = SPAI_ERR_DEVICE;
+    }
+    for (auto &ev : L->ev_dz)
+        if (rc == SPAI_OK && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            set_error("learner: event creation failed");
+            rc = SPAI_ERR_DEVICE;
+        }
     chk(L->run_buf.alloc(ridx.size()));
     if (rc == SPAI_OK) {
         hipStream_t st = e->stream;
@@ -776,9 +798,14 @@ int learner_create(spai_engine *e, int blocks, int hidden, const float *params, 
 void learner_destroy(spai_learner *L) {
     if (!L) return;
     if (L->eng) (void)hipStreamSynchronize(L->eng->stream);
+    if (L->wg_stream) (void)hipStreamSynchronize(L->wg_stream);
     if (L->comm) (void)ncclCommDestroy((ncclComm_t)L->comm);
+    for (hipEvent_t ev : L->ev_dz)
+        if (ev) (void)hipEventDestroy(ev);
+    if (L->ev_wg_done) (void)hipEventDestroy(L->ev_wg_done);
+    if (L->wg_stream) (void)hipStreamDestroy(L->wg_stream);
     L->pack_desc.release();
-    for (auto *b : {&L->p, &L->g, &L->bsum, &L->m, &L->v, &L->wt, &L->x_in, &L->pi, &L->zv, &L->d0, &L->d1, &L->d2, &L->dlogits,
+    for (auto *b : {&L->p, &L->g, &L->bsum, &L->m, &L->v, &L->wt, &L->x_in, &L->pi, &L->zv, &L->d0, &L->d1, &L->dlogits,
                     &L->dpre, &L->loss_terms, &L->wpart, &L->run_buf})
         b->release();
     L->run_idx.release();
@@ -826,23 +853,35 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
 
     // ---------------- backward
     // heads: linears -> relu/BN -> conv; dh (d0) = dgrad(policy) + dgrad(value)
-    k_linear_bwd_w<<<blocks_of(7 * 32 * kCells), kThreads, 0, st>>>(L->a[pol].p, L->dlogits.p, (int)B, 7, 32 * kCells,
+    k_linear_bwd_w<<<(7 * 32 * kCells + 63) / 64, kThreads, 0, st>>>(L->a[pol].p, L->dlogits.p, (int)B, 7, 32 * kCells,
                                                                      G + L->pol_w, G + L->pol_b);
     k_linear_bwd_x<<<blocks_of((size_t)B * 32 * kCells), kThreads, 0, st>>>(L->dlogits.p, P + L->pol_w, (int)B, 7,
                                                                              32 * kCells, L->d1.p);
-    auto bn_conv_bwd = [&](int l, const float *da, const float *in, float *dx, bool acc) {
+    // conv l's dz (written over z[l] by k_bn_bwd) feeds its data gradient here and
+    // its weight gradient on wg_stream; nothing rewrites z[l] before the next step
+    auto wgrad_async = [&](int l, const float *in) {
+        const spai_learner::Conv &c = L->convs[l];
+        if (crc != SPAI_OK) return;
+        if (hipEventRecord(L->ev_dz[l], st) != hipSuccess || hipStreamWaitEvent(L->wg_stream, L->ev_dz[l], 0) != hipSuccess) {
+            set_error("learner: event record/wait failed");
+            crc = SPAI_ERR_DEVICE;
+            return;
+        }
+        crc = launch_wgrad(L, in, c.ci, L->z[l].p, c.co, (int)B, G + c.w, L->wg_stream);
+    };
+    auto bn_conv_bwd = [&](int l, const float *da, const float *in, float *dx, bool acc, float *dy_out) {
         const spai_learner::Conv &c = L->convs[l];
         k_bn_bwd<<<c.co, kBn, 0, st>>>(da, L->a[l].p, L->z[l].p, c.co, (int)B, L->mean[l].p, L->invstd[l].p,
-                                       P + c.g, G + c.g, G + c.be, G + c.b, L->d2.p, nullptr);
-        if (crc == SPAI_OK) crc = launch_wgrad(L, in, c.ci, L->d2.p, c.co, (int)B, G + c.w, st);
-        if (dx && crc == SPAI_OK) crc = launch_conv(L->d2.p, c.co, W + c.wkd, nullptr, c.ci, dx, (int)B, acc, st);
+                                       P + c.g, G + c.g, G + c.be, G + c.b, L->z[l].p, dy_out);
+        wgrad_async(l, in);
+        if (dx && crc == SPAI_OK) crc = launch_conv(L->z[l].p, c.co, W + c.wkd, nullptr, c.ci, dx, (int)B, acc, st);
     };
-    bn_conv_bwd(pol, L->d1.p, h, L->d0.p, false);
-    k_linear_bwd_w<<<blocks_of(3 * kCells), kThreads, 0, st>>>(L->a[val].p, L->dpre.p, (int)B, 1, 3 * kCells,
+    bn_conv_bwd(pol, L->d1.p, h, L->d0.p, false, nullptr);
+    k_linear_bwd_w<<<(3 * kCells + 63) / 64, kThreads, 0, st>>>(L->a[val].p, L->dpre.p, (int)B, 1, 3 * kCells,
                                                                 G + L->val_w, G + L->val_b);
     k_linear_bwd_x<<<blocks_of((size_t)B * 3 * kCells), kThreads, 0, st>>>(L->dpre.p, P + L->val_w, (int)B, 1,
                                                                             3 * kCells, L->d1.p);
-    bn_conv_bwd(val, L->d1.p, h, L->d0.p, true);
+    bn_conv_bwd(val, L->d1.p, h, L->d0.p, true, nullptr);
     // residual blocks in reverse; d0 holds dL/d(block output)
     for (int k = L->blocks - 1; k >= 0; --k) {
         const int l1 = 1 + 2 * k, l2 = 2 + 2 * k;
@@ -850,21 +889,20 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
         // BN2/conv2 backward: dt = d(out) * (out > 0) is the gradient of the pre-ReLU sum, shared
         // by BN2 and the skip path (k_bn_bwd also writes it to d1); conv2's input is a[l1]; its
         // data gradient overwrites d0 with dL/d(relu1 output)
-        {
-            const spai_learner::Conv &c = L->convs[l2];
-            k_bn_bwd<<<c.co, kBn, 0, st>>>(L->d0.p, L->a[l2].p, L->z[l2].p, c.co, (int)B, L->mean[l2].p,
-                                           L->invstd[l2].p, P + c.g, G + c.g, G + c.be, G + c.b, L->d2.p, L->d1.p);
-            if (crc == SPAI_OK) crc = launch_wgrad(L, L->a[l1].p, c.ci, L->d2.p, c.co, (int)B, G + c.w, st);
-            if (crc == SPAI_OK) crc = launch_conv(L->d2.p, c.co, W + c.wkd, nullptr, c.ci, L->d0.p, (int)B, false, st);
-        }
+        bn_conv_bwd(l2, L->d0.p, L->a[l1].p, L->d0.p, false, L->d1.p);
         // BN1/conv1 backward: da = d0 (gradient wrt relu1 output), mask a[l1]; its input is hin;
         // dgrad accumulates into d1 (= dt, the skip gradient) -> d(block input)
-        bn_conv_bwd(l1, L->d0.p, hin, L->d1.p, true);
+        bn_conv_bwd(l1, L->d0.p, hin, L->d1.p, true, nullptr);
         std::swap(L->d0, L->d1);   // d0 = dL/d(block input)
     }
     // stem: no data gradient
-    bn_conv_bwd(0, L->d0.p, L->x_in.p, nullptr, false);
-
+    bn_conv_bwd(0, L->d0.p, L->x_in.p, nullptr, false, nullptr);
+    // join: every weight gradient is in G before the reduction and Adam
+    if (crc == SPAI_OK && (hipEventRecord(L->ev_wg_done, L->wg_stream) != hipSuccess ||
+                           hipStreamWaitEvent(st, L->ev_wg_done, 0) != hipSuccess)) {
+        set_error("learner: event record/wait failed");
+        crc = SPAI_ERR_DEVICE;
+    }
     SPAI_TRY(crc);
     // ---------------- cross-rank reduction + Adam
     // The global step's gradient is the mean over every rank's samples: each rank

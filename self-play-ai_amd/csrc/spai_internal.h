@@ -151,10 +151,15 @@ struct spai_learner {
     int n_pack = 0;
     spai::DevBuf<float> x_in, pi, zv;   // batch
     std::vector<spai::DevBuf<float>> z, a, mean, invstd;   // per conv layer
-    spai::DevBuf<float> d0, d1, d2;     // backward scratch [B][64][42]
+    spai::DevBuf<float> d0, d1;         // backward scratch [B][64][42]
     spai::DevBuf<float> dlogits, dpre, loss_terms, wpart;
     spai::DevBuf<uint32_t> run_idx;     // BN running-stat offsets (for the cross-rank average)
     spai::DevBuf<float> run_buf;
+    // backward: the weight gradients run on wg_stream beside the data-gradient
+    // chain (event per conv layer: its dz is ready), joined before the reduction
+    hipStream_t wg_stream = nullptr;
+    std::vector<hipEvent_t> ev_dz;
+    hipEvent_t ev_wg_done = nullptr;
     void *comm = nullptr;            // ncclComm_t (learner.hip)
     int rank = 0, world = 1;
 };
