@@ -598,9 +598,15 @@ namespace {
 int learner_alloc_batch(spai_learner *L, uint32_t B) {
     if (B <= L->max_batch) return SPAI_OK;
     const size_t act = (size_t)B * std::max(L->hidden, 32) * kCells;   // also the 32-channel policy head
-    SPAI_TRY(L->x_in.alloc((size_t)B * 3 * kCells));
-    SPAI_TRY(L->pi.alloc((size_t)B * 7));
-    SPAI_TRY(L->zv.alloc(B));
+    SPAI_TRY(L->batch_in.alloc((size_t)B * (3 * kCells + 8)));
+    if (L->stage) (void)hipHostFree(L->stage);
+    L->stage = nullptr;
+    if (hipHostMalloc((void **)&L->stage, (size_t)B * (3 * kCells + 10) * sizeof(float), hipHostMallocDefault) !=
+        hipSuccess) {
+        L->stage = nullptr;
+        set_error("learner: pinned staging allocation failed");
+        return SPAI_ERR_DEVICE;
+    }
     for (size_t l = 0; l < L->convs.size(); ++l) {
         SPAI_TRY(L->z[l].alloc((size_t)B * L->convs[l].co * kCells));
         SPAI_TRY(L->a[l].alloc((size_t)B * L->convs[l].co * kCells));
@@ -805,7 +811,8 @@ void learner_destroy(spai_learner *L) {
     if (L->ev_wg_done) (void)hipEventDestroy(L->ev_wg_done);
     if (L->wg_stream) (void)hipStreamDestroy(L->wg_stream);
     L->pack_desc.release();
-    for (auto *b : {&L->p, &L->g, &L->bsum, &L->m, &L->v, &L->wt, &L->x_in, &L->pi, &L->zv, &L->d0, &L->d1, &L->dlogits,
+    if (L->stage) (void)hipHostFree(L->stage);
+    for (auto *b : {&L->p, &L->g, &L->bsum, &L->m, &L->v, &L->wt, &L->batch_in, &L->d0, &L->d1, &L->dlogits,
                     &L->dpre, &L->loss_terms, &L->wpart, &L->run_buf})
         b->release();
     L->run_idx.release();
@@ -820,9 +827,13 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
     SPAI_TRY(learner_alloc_batch(L, B));
     hipStream_t st = L->eng->stream;
     float *P = L->p.p, *G = L->g.p;
-    SPAI_HIP(hipMemcpyAsync(L->x_in.p, states, (size_t)B * 3 * kCells * 4, hipMemcpyHostToDevice, st));
-    SPAI_HIP(hipMemcpyAsync(L->pi.p, policies, (size_t)B * 7 * 4, hipMemcpyHostToDevice, st));
-    SPAI_HIP(hipMemcpyAsync(L->zv.p, values, (size_t)B * 4, hipMemcpyHostToDevice, st));
+    // one DMA from pinned staging for the whole batch
+    const size_t nin = (size_t)B * (3 * kCells + 8);
+    std::memcpy(L->stage, states, (size_t)B * 3 * kCells * 4);
+    std::memcpy(L->stage + (size_t)B * 3 * kCells, policies, (size_t)B * 7 * 4);
+    std::memcpy(L->stage + (size_t)B * (3 * kCells + 7), values, (size_t)B * 4);
+    SPAI_HIP(hipMemcpyAsync(L->batch_in.p, L->stage, nin * 4, hipMemcpyHostToDevice, st));
+    const float *x_in = L->batch_in.p, *pi_in = x_in + (size_t)B * 3 * kCells, *z_in = pi_in + (size_t)B * 7;
     SPAI_HIP(hipMemsetAsync(G, 0, L->n_params * 4, st));
     const float eps = L->cfg.bn_eps, mom = L->cfg.bn_momentum;
     const size_t nl = L->convs.size();
@@ -838,7 +849,7 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
         k_bn_fwd<<<c.co, kBn, 0, st>>>(L->z[l].p, c.co, (int)B, eps, mom, L->mean[l].p, L->invstd[l].p, P + c.mu,
                                        P + c.var, P + c.g, P + c.be, res, L->a[l].p);
     };
-    conv_bn_act(0, L->x_in.p, nullptr);
+    conv_bn_act(0, x_in, nullptr);
     const float *h = L->a[0].p;
     for (int k = 0; k < L->blocks; ++k) {   // relu(h + BN(conv(relu(BN(conv(h)))))) (model/mod.rs:152-165)
         conv_bn_act(1 + 2 * k, h, nullptr);
@@ -848,7 +859,7 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
     conv_bn_act(pol, h, nullptr);
     conv_bn_act(val, h, nullptr);
     k_heads_loss<<<B, kThreads, 0, st>>>(L->a[pol].p, L->a[val].p, P + L->pol_w, P + L->pol_b, P + L->val_w,
-                                         P + L->val_b, L->pi.p, L->zv.p, (int)B, L->dlogits.p, L->dpre.p,
+                                         P + L->val_b, pi_in, z_in, (int)B, L->dlogits.p, L->dpre.p,
                                          L->loss_terms.p);
 
     // ---------------- backward
@@ -896,7 +907,7 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
         std::swap(L->d0, L->d1);   // d0 = dL/d(block input)
     }
     // stem: no data gradient
-    bn_conv_bwd(0, L->d0.p, L->x_in.p, nullptr, false, nullptr);
+    bn_conv_bwd(0, L->d0.p, x_in, nullptr, false, nullptr);
     // join: every weight gradient is in G before the reduction and Adam
     if (crc == SPAI_OK && (hipEventRecord(L->ev_wg_done, L->wg_stream) != hipSuccess ||
                            hipStreamWaitEvent(st, L->ev_wg_done, 0) != hipSuccess)) {
@@ -938,8 +949,8 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
         k_scatter_scaled<<<blocks_of(nr), kThreads, 0, st>>>(L->run_buf.p, L->run_idx.p, nr, 1.0f / (float)L->world, P);
     }
     SPAI_HIP(hipGetLastError());
-    std::vector<float> terms((size_t)B * 2);
-    SPAI_HIP(hipMemcpyAsync(terms.data(), L->loss_terms.p, terms.size() * 4, hipMemcpyDeviceToHost, st));
+    float *terms = L->stage + nin;   // the staged inputs were consumed by the DMA above (stream order)
+    SPAI_HIP(hipMemcpyAsync(terms, L->loss_terms.p, (size_t)B * 2 * 4, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipStreamSynchronize(st));
     double lp = 0, lv = 0;   // fixed-order host sums
     for (uint32_t b = 0; b < B; ++b) {

@@ -149,7 +149,8 @@ struct spai_learner {
     spai::DevBuf<float> wt;             // packed conv matrices (forward and data gradient), once per step
     spai::DevBuf<uint32_t> pack_desc;   // their table (k_pack_all)
     int n_pack = 0;
-    spai::DevBuf<float> x_in, pi, zv;   // batch
+    spai::DevBuf<float> batch_in;       // batch [x: B*126 | pi: B*7 | z: B]
+    float *stage = nullptr;             // pinned host copy of it, then the loss terms [B*2]
     std::vector<spai::DevBuf<float>> z, a, mean, invstd;   // per conv layer
     spai::DevBuf<float> d0, d1;         // backward scratch [B][64][42]
     spai::DevBuf<float> dlogits, dpre, loss_terms, wpart;
