@@ -404,9 +404,16 @@ __device__ __forceinline__ void forward_body(uint8_t *smem, uint32_t count, uint
     }
 }
 
-// P = 2 positions per workgroup, or 1 when there are no more positions than
-// CUs (the small batches of a game's tail: the same work per CU, half the
-// latency).  A position's results do not depend on P.
+// Up to n_cu workgroups, one per CU (140 KiB of LDS each).  With no more
+// positions than CUs, one position per workgroup (P = 1).  Otherwise, with
+// m = ceil(count / n_cu) positions on the busiest CU:
+//  * m even: P = 2 passes over slots 2w, 2w + 2 n_cu, ... (m / 2 passes);
+//  * m odd: the count is split evenly (q or q + 1 positions per workgroup),
+//    run as P = 2 passes plus one P = 1 pass: 600 positions take a P = 2 and a
+//    P = 1 pass instead of two P = 2 passes (+25 % at 520-700 positions;
+//    profiles/r02/chess/split_ab.txt).  For even m the even split measured
+//    slower (-7..-11 %: more workgroups stream the weights for no fewer passes).
+// A position's results do not depend on P or on its workgroup.
 __global__ void __launch_bounds__(kThreads, 1)
     k_chess_forward(const uint32_t *__restrict__ d_count, uint32_t max_n, uint32_t n_cu,
                     const uint16_t *__restrict__ x, NetW W, float *__restrict__ logits, float *__restrict__ value) {
@@ -414,14 +421,29 @@ __global__ void __launch_bounds__(kThreads, 1)
     const uint32_t count = d_count ? min(*d_count, max_n) : max_n;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t w = blockIdx.x;
     if (count <= n_cu) {
-        if (blockIdx.x >= count) return;
-        forward_body<1>(smem, count, blockIdx.x, x, W, logits, value, tid, lane, wave);
-    } else {
-        const uint32_t slot0 = blockIdx.x * 2;
-        if (slot0 >= count) return;
-        forward_body<2>(smem, count, slot0, x, W, logits, value, tid, lane, wave);
+        if (w >= count) return;
+        forward_body<1>(smem, count, w, x, W, logits, value, tid, lane, wave);
+        return;
     }
+    if (w >= n_cu) return;
+    const uint32_t m = (count + n_cu - 1) / n_cu;
+    if ((m & 1) == 0) {
+        for (uint32_t slot0 = 2 * w; slot0 < count; slot0 += 2 * n_cu) {
+            forward_body<2>(smem, count, slot0, x, W, logits, value, tid, lane, wave);
+            __syncthreads();   // the next pass restages the LDS
+        }
+        return;
+    }
+    const uint32_t q = count / n_cu, r = count % n_cu;
+    uint32_t lo = w * q + min(w, r);
+    const uint32_t hi = lo + q + (w < r ? 1u : 0u);
+    for (; lo + 2 <= hi; lo += 2) {
+        forward_body<2>(smem, count, lo, x, W, logits, value, tid, lane, wave);
+        __syncthreads();
+    }
+    if (lo < hi) forward_body<1>(smem, count, lo, x, W, logits, value, tid, lane, wave);
 }
 
 // f32 [n][19][8][8] -> bf16 [n][64][kInCh]
@@ -645,8 +667,9 @@ static NetW weights_of(const spai_chess_net *n) {
 int net_eval(spai_chess_net *net, hipStream_t st, const uint32_t *d_count, uint32_t max_n, const uint16_t *x,
              float *logits, float *value) {
     if (!max_n) return SPAI_OK;
-    k_chess_forward<<<max_n, kThreads, 0, st>>>(d_count, max_n, (uint32_t)net->eng->n_cu, x, weights_of(net), logits,
-                                                value);
+    const uint32_t n_cu = (uint32_t)net->eng->n_cu;
+    k_chess_forward<<<std::min(max_n, n_cu), kThreads, 0, st>>>(d_count, max_n, n_cu, x, weights_of(net), logits,
+                                                               value);
     SPAI_HIP(hipGetLastError());
     return SPAI_OK;
 }
