@@ -19,6 +19,7 @@
 // mcts.rs:161-192, done only when needed; the root keeps N and W, quirk Q4).
 #include <algorithm>
 #include <chrono>
+#include <memory>
 #include <cmath>
 #include <cstring>
 
@@ -811,12 +812,20 @@ int selfplay_run(spai_chess *e, uint32_t n_games, uint64_t gid_base, spai_chess_
     std::vector<Board> nb;
     std::vector<float> enc, pol, val;
     std::vector<uint16_t> mvs;
+    // optional per-move trace (diagnostics): SPAI_TRACE_MOVES=<csv path>, lines of
+    // move, active games, leaves evaluated, seconds (search + root statistics)
+    std::unique_ptr<FILE, int (*)(FILE *)> trace(nullptr, &std::fclose);
+    if (const char *tp = std::getenv("SPAI_TRACE_MOVES")) trace.reset(std::fopen(tp, "a"));
     while (!act.empty()) {
         const uint32_t na = (uint32_t)act.size();
+        const auto tm0 = std::chrono::steady_clock::now();
         SPAI_HIP(hipMemcpyAsync(e->active.p, act.data(), 4 * na, hipMemcpyHostToDevice, e->stream));
         double ev = 0;
         SPAI_TRY(run_search(e, na, sims, &ev));
         SPAI_TRY(root_stats(e, na));
+        if (trace)
+            std::fprintf(trace.get(), "%llu,%u,%.0f,%.6f\n", (unsigned long long)move_no, na, ev,
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - tm0).count());
         evals += ev;
         sims_done += (double)na * sims;
         moves += 1;
