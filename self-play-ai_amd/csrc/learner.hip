@@ -552,11 +552,13 @@ __global__ void k_linear_bwd_x(const float *__restrict__ dy, const float *__rest
 // ------------------------------------------------------------------ Adam (torch semantics)
 // m = b1 m + (1-b1) g;  v = b2 v + (1-b2) g^2;
 // p -= lr / (1 - b1^t) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)      (g scaled by gscale)
+// bc = {1 - b1^t, sqrt(1 - b2^t)} for this step (host-computed, staged with the batch)
 __global__ void k_adam(float *__restrict__ p, const float *__restrict__ g, float *__restrict__ m,
                        float *__restrict__ v, size_t n, float gscale, float lr, float b1, float b2, float eps,
-                       float bc1, float bc2_sqrt) {
+                       const float *__restrict__ bc) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    const float bc1 = bc[0], bc2_sqrt = bc[1];
     const float gi = g[i] * gscale;
     const float mi = b1 * m[i] + (1.0f - b1) * gi;
     const float vi = b2 * v[i] + (1.0f - b2) * gi * gi;
@@ -598,10 +600,10 @@ namespace {
 int learner_alloc_batch(spai_learner *L, uint32_t B) {
     if (B <= L->max_batch) return SPAI_OK;
     const size_t act = (size_t)B * std::max(L->hidden, 32) * kCells;   // also the 32-channel policy head
-    SPAI_TRY(L->batch_in.alloc((size_t)B * (3 * kCells + 8)));
+    SPAI_TRY(L->batch_in.alloc((size_t)B * (3 * kCells + 8) + 2));
     if (L->stage) (void)hipHostFree(L->stage);
     L->stage = nullptr;
-    if (hipHostMalloc((void **)&L->stage, (size_t)B * (3 * kCells + 10) * sizeof(float), hipHostMallocDefault) !=
+    if (hipHostMalloc((void **)&L->stage, ((size_t)B * (3 * kCells + 10) + 2) * sizeof(float), hipHostMallocDefault) !=
         hipSuccess) {
         L->stage = nullptr;
         set_error("learner: pinned staging allocation failed");
@@ -821,19 +823,12 @@ void learner_destroy(spai_learner *L) {
     delete L;
 }
 
-int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const float *policies, const float *values,
-                        float *loss3) {
-    SPAI_CHECK(B >= 1, SPAI_ERR_INVALID, "train_batch: empty batch");
-    SPAI_TRY(learner_alloc_batch(L, B));
-    hipStream_t st = L->eng->stream;
+// Everything of one train step after the batch upload: gradients zeroed, weights
+// packed, forward, loss, backward (weight gradients on wg_stream), the cross-rank
+// reduction when there is a communicator, Adam.  Launch-only (no host sync).
+int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in, const float *pi_in,
+                 const float *z_in, const float *bc) {
     float *P = L->p.p, *G = L->g.p;
-    // one DMA from pinned staging for the whole batch
-    const size_t nin = (size_t)B * (3 * kCells + 8);
-    std::memcpy(L->stage, states, (size_t)B * 3 * kCells * 4);
-    std::memcpy(L->stage + (size_t)B * 3 * kCells, policies, (size_t)B * 7 * 4);
-    std::memcpy(L->stage + (size_t)B * (3 * kCells + 7), values, (size_t)B * 4);
-    SPAI_HIP(hipMemcpyAsync(L->batch_in.p, L->stage, nin * 4, hipMemcpyHostToDevice, st));
-    const float *x_in = L->batch_in.p, *pi_in = x_in + (size_t)B * 3 * kCells, *z_in = pi_in + (size_t)B * 7;
     SPAI_HIP(hipMemsetAsync(G, 0, L->n_params * 4, st));
     const float eps = L->cfg.bn_eps, mom = L->cfg.bn_momentum;
     const size_t nl = L->convs.size();
@@ -933,12 +928,8 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
             return SPAI_ERR_DEVICE;
         }
     }
-    L->step += 1;
-    const double t = (double)L->step;
-    const float bc1 = (float)(1.0 - std::pow((double)L->cfg.beta1, t));
-    const float bc2s = (float)std::sqrt(1.0 - std::pow((double)L->cfg.beta2, t));
     k_adam<<<blocks_of(L->n_params), kThreads, 0, st>>>(P, G, L->m.p, L->v.p, L->n_params, gscale, L->cfg.lr,
-                                                        L->cfg.beta1, L->cfg.beta2, L->cfg.eps, bc1, bc2s);
+                                                        L->cfg.beta1, L->cfg.beta2, L->cfg.eps, bc);
     if (L->comm) {   // average the BN running statistics so replicas stay identical
         const uint32_t nr = (uint32_t)L->run_idx.n;
         k_gather<<<blocks_of(nr), kThreads, 0, st>>>(P, L->run_idx.p, nr, L->run_buf.p);
@@ -949,7 +940,30 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
         k_scatter_scaled<<<blocks_of(nr), kThreads, 0, st>>>(L->run_buf.p, L->run_idx.p, nr, 1.0f / (float)L->world, P);
     }
     SPAI_HIP(hipGetLastError());
-    float *terms = L->stage + nin;   // the staged inputs were consumed by the DMA above (stream order)
+    return SPAI_OK;
+}
+
+int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const float *policies, const float *values,
+                        float *loss3) {
+    SPAI_CHECK(B >= 1, SPAI_ERR_INVALID, "train_batch: empty batch");
+    SPAI_TRY(learner_alloc_batch(L, B));
+    hipStream_t st = L->eng->stream;
+    // one DMA from pinned staging for the whole batch and this step's Adam bias corrections
+    const size_t nin = (size_t)B * (3 * kCells + 8);
+    L->step += 1;
+    const double t = (double)L->step;
+    L->stage[nin] = (float)(1.0 - std::pow((double)L->cfg.beta1, t));
+    L->stage[nin + 1] = (float)std::sqrt(1.0 - std::pow((double)L->cfg.beta2, t));
+    std::memcpy(L->stage, states, (size_t)B * 3 * kCells * 4);
+    std::memcpy(L->stage + (size_t)B * 3 * kCells, policies, (size_t)B * 7 * 4);
+    std::memcpy(L->stage + (size_t)B * (3 * kCells + 7), values, (size_t)B * 4);
+    SPAI_HIP(hipMemcpyAsync(L->batch_in.p, L->stage, (nin + 2) * 4, hipMemcpyHostToDevice, st));
+    const float *x_in = L->batch_in.p, *pi_in = x_in + (size_t)B * 3 * kCells, *z_in = pi_in + (size_t)B * 7;
+    const float *bc = L->batch_in.p + nin;
+    // (a hipGraph of this step, captured once per batch size, measured 130k
+    // samples/s against 162k eager: profiles/r02/learner/graph_ab.txt)
+    SPAI_TRY(enqueue_step(L, B, st, x_in, pi_in, z_in, bc));
+    float *terms = L->stage + nin + 2;   // the staged inputs were consumed by the DMA above (stream order)
     SPAI_HIP(hipMemcpyAsync(terms, L->loss_terms.p, (size_t)B * 2 * 4, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipStreamSynchronize(st));
     double lp = 0, lv = 0;   // fixed-order host sums
