@@ -619,7 +619,8 @@ int learner_alloc_batch(spai_learner *L, uint32_t B) {
     SPAI_TRY(L->dpre.alloc(B));
     SPAI_TRY(L->loss_terms.alloc((size_t)B * 2));
     const size_t cmax = (size_t)std::max(L->hidden, 32);
-    SPAI_TRY(L->wpart.alloc((size_t)B * cmax * 9 * round4(L->hidden)));   // per-sample weight-gradient partials
+    for (auto &w : L->wpart_side)   // weight-gradient partials per chunk (one buffer per side stream)
+        SPAI_TRY(w.alloc((size_t)((B + kWgSamples - 1) / kWgSamples) * cmax * 9 * round4(L->hidden)));
     L->max_batch = B;
     return SPAI_OK;
 }
@@ -671,18 +672,18 @@ int launch_conv(const float *in, int cin, const float *wk, const float *bias, in
 }
 
 // dW, db of one conv: chunk partials on f32 MFMA, then a fixed-order sum over the chunks
-int launch_wgrad(spai_learner *L, const float *x, int cin, const float *dz, int cout, int B, float *dw, hipStream_t st) {
+int launch_wgrad(float *wpart, const float *x, int cin, const float *dz, int cout, int B, float *dw, hipStream_t st) {
     const int cinp = round4(cin), nk = (9 * cinp + 15) / 16, ntiles = (round16(cout) / 16) * nk;
     const int groups = std::max(1, (ntiles + 4 * kWgMaxTiles - 1) / (4 * kWgMaxTiles));
     const int chunks = (B + kWgSamples - 1) / kWgSamples;
     const size_t lds = ((size_t)cinp * kPlane + (size_t)round16(cout) * 44) * sizeof(float);
     const dim3 grid(chunks, groups);
     switch (cinp) {
-    case 4: k_wgrad_mfma<4><<<grid, kThreads, lds, st>>>(x, cin, dz, cout, B, groups, L->wpart.p); break;
-    case 64: k_wgrad_mfma<64><<<grid, kThreads, lds, st>>>(x, cin, dz, cout, B, groups, L->wpart.p); break;
+    case 4: k_wgrad_mfma<4><<<grid, kThreads, lds, st>>>(x, cin, dz, cout, B, groups, wpart); break;
+    case 64: k_wgrad_mfma<64><<<grid, kThreads, lds, st>>>(x, cin, dz, cout, B, groups, wpart); break;
     default: set_error("learner wgrad: %d input channels not built", cin); return SPAI_ERR_UNSUPPORTED;
     }
-    k_wgrad_reduce<<<blocks_of((size_t)cout * 9 * cinp), kThreads, 0, st>>>(L->wpart.p, chunks, cin, cout, dw);
+    k_wgrad_reduce<<<blocks_of((size_t)cout * 9 * cinp), kThreads, 0, st>>>(wpart, chunks, cin, cout, dw);
     return SPAI_OK;
 }
 
@@ -774,11 +775,12 @@ int learner_create(spai_engine *e, int blocks, int hidden, const float *params, 
     }
     chk(L->run_idx.alloc(ridx.size()));
     L->ev_dz.assign(L->convs.size(), nullptr);
-    if (hipStreamCreateWithFlags(&L->wg_stream, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&L->ev_wg_done, hipEventDisableTiming) != hipSuccess) {
-        set_error("learner: stream/event creation failed");
-        rc = SPAI_ERR_DEVICE;
-    }
+    for (int k = 0; k < spai_learner::kWgStreams; ++k)
+        if (rc == SPAI_OK && (hipStreamCreateWithFlags(&L->wg_stream[k], hipStreamNonBlocking) != hipSuccess ||
+                              hipEventCreateWithFlags(&L->ev_wg_done[k], hipEventDisableTiming) != hipSuccess)) {
+            set_error("learner: stream/event creation failed");
+            rc = SPAI_ERR_DEVICE;
+        }
     for (auto &ev : L->ev_dz)
         if (rc == SPAI_OK && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
             set_error("learner: event creation failed");
@@ -806,16 +808,20 @@ int learner_create(spai_engine *e, int blocks, int hidden, const float *params, 
 void learner_destroy(spai_learner *L) {
     if (!L) return;
     if (L->eng) (void)hipStreamSynchronize(L->eng->stream);
-    if (L->wg_stream) (void)hipStreamSynchronize(L->wg_stream);
+    for (hipStream_t ws : L->wg_stream)
+        if (ws) (void)hipStreamSynchronize(ws);
     if (L->comm) (void)ncclCommDestroy((ncclComm_t)L->comm);
     for (hipEvent_t ev : L->ev_dz)
         if (ev) (void)hipEventDestroy(ev);
-    if (L->ev_wg_done) (void)hipEventDestroy(L->ev_wg_done);
-    if (L->wg_stream) (void)hipStreamDestroy(L->wg_stream);
+    for (int k = 0; k < spai_learner::kWgStreams; ++k) {
+        if (L->ev_wg_done[k]) (void)hipEventDestroy(L->ev_wg_done[k]);
+        if (L->wg_stream[k]) (void)hipStreamDestroy(L->wg_stream[k]);
+        L->wpart_side[k].release();
+    }
     L->pack_desc.release();
     if (L->stage) (void)hipHostFree(L->stage);
     for (auto *b : {&L->p, &L->g, &L->bsum, &L->m, &L->v, &L->wt, &L->batch_in, &L->d0, &L->d1, &L->dlogits,
-                    &L->dpre, &L->loss_terms, &L->wpart, &L->run_buf})
+                    &L->dpre, &L->loss_terms, &L->run_buf})
         b->release();
     L->run_idx.release();
     for (auto *vec : {&L->z, &L->a, &L->mean, &L->invstd})
@@ -824,7 +830,7 @@ void learner_destroy(spai_learner *L) {
 }
 
 // Everything of one train step after the batch upload: gradients zeroed, weights
-// packed, forward, loss, backward (weight gradients on wg_stream), the cross-rank
+// packed, forward, loss, backward (weight gradients on the side streams), the cross-rank
 // reduction when there is a communicator, Adam.  Launch-only (no host sync).
 int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in, const float *pi_in,
                  const float *z_in, const float *bc) {
@@ -864,16 +870,22 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
     k_linear_bwd_x<<<blocks_of((size_t)B * 32 * kCells), kThreads, 0, st>>>(L->dlogits.p, P + L->pol_w, (int)B, 7,
                                                                              32 * kCells, L->d1.p);
     // conv l's dz (written over z[l] by k_bn_bwd) feeds its data gradient here and
-    // its weight gradient on wg_stream; nothing rewrites z[l] before the next step
+    // its weight gradient on a side stream; nothing rewrites z[l] before the next step
+#ifndef SPAI_WG_SIDE
+#define SPAI_WG_SIDE spai_learner::kWgStreams
+#endif
+    int side = 0;
     auto wgrad_async = [&](int l, const float *in) {
         const spai_learner::Conv &c = L->convs[l];
         if (crc != SPAI_OK) return;
-        if (hipEventRecord(L->ev_dz[l], st) != hipSuccess || hipStreamWaitEvent(L->wg_stream, L->ev_dz[l], 0) != hipSuccess) {
+        const int k = side++ % SPAI_WG_SIDE;
+        if (hipEventRecord(L->ev_dz[l], st) != hipSuccess ||
+            hipStreamWaitEvent(L->wg_stream[k], L->ev_dz[l], 0) != hipSuccess) {
             set_error("learner: event record/wait failed");
             crc = SPAI_ERR_DEVICE;
             return;
         }
-        crc = launch_wgrad(L, in, c.ci, L->z[l].p, c.co, (int)B, G + c.w, L->wg_stream);
+        crc = launch_wgrad(L->wpart_side[k].p, in, c.ci, L->z[l].p, c.co, (int)B, G + c.w, L->wg_stream[k]);
     };
     auto bn_conv_bwd = [&](int l, const float *da, const float *in, float *dx, bool acc, float *dy_out) {
         const spai_learner::Conv &c = L->convs[l];
@@ -904,11 +916,12 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
     // stem: no data gradient
     bn_conv_bwd(0, L->d0.p, x_in, nullptr, false, nullptr);
     // join: every weight gradient is in G before the reduction and Adam
-    if (crc == SPAI_OK && (hipEventRecord(L->ev_wg_done, L->wg_stream) != hipSuccess ||
-                           hipStreamWaitEvent(st, L->ev_wg_done, 0) != hipSuccess)) {
-        set_error("learner: event record/wait failed");
-        crc = SPAI_ERR_DEVICE;
-    }
+    for (int k = 0; k < SPAI_WG_SIDE && crc == SPAI_OK; ++k)
+        if (hipEventRecord(L->ev_wg_done[k], L->wg_stream[k]) != hipSuccess ||
+            hipStreamWaitEvent(st, L->ev_wg_done[k], 0) != hipSuccess) {
+            set_error("learner: event record/wait failed");
+            crc = SPAI_ERR_DEVICE;
+        }
     SPAI_TRY(crc);
     // ---------------- cross-rank reduction + Adam
     // The global step's gradient is the mean over every rank's samples: each rank

@@ -153,14 +153,18 @@ struct spai_learner {
     float *stage = nullptr;             // pinned host copy of it, then the loss terms [B*2]
     std::vector<spai::DevBuf<float>> z, a, mean, invstd;   // per conv layer
     spai::DevBuf<float> d0, d1;         // backward scratch [B][64][42]
-    spai::DevBuf<float> dlogits, dpre, loss_terms, wpart;
+    spai::DevBuf<float> dlogits, dpre, loss_terms;
     spai::DevBuf<uint32_t> run_idx;     // BN running-stat offsets (for the cross-rank average)
     spai::DevBuf<float> run_buf;
-    // backward: the weight gradients run on wg_stream beside the data-gradient
-    // chain (event per conv layer: its dz is ready), joined before the reduction
-    hipStream_t wg_stream = nullptr;
+    // backward: the weight gradients run on kWgStreams side streams (layers dealt
+    // round-robin) beside the data-gradient chain (an event per conv layer: its dz
+    // is ready), each with its own partials buffer, joined before the reduction.
+    // One: two measured 163k against 167k samples/s (profiles/r02/learner/side_streams.txt)
+    static constexpr int kWgStreams = 1;
+    hipStream_t wg_stream[kWgStreams] = {};
     std::vector<hipEvent_t> ev_dz;
-    hipEvent_t ev_wg_done = nullptr;
+    hipEvent_t ev_wg_done[kWgStreams] = {};
+    spai::DevBuf<float> wpart_side[kWgStreams];
     void *comm = nullptr;            // ncclComm_t (learner.hip)
     int rank = 0, world = 1;
 };
