@@ -637,16 +637,15 @@ int launch_conv_t(int B, size_t lds, hipStream_t st, const float *in, int cin, c
                   int cout, float *out, int acc) {
     constexpr int ks = 9 * CINP / 4;
     const int nt = round16(cout) / 16;
-#ifdef SPAI_CONV_ROWS
-    if (nt == 4 && CINP >= 32) {   // one workgroup per (sample, position tile): the unsplit K order
-        k_conv_mfma<CINP, 4, 1><<<dim3(B, 3), kThreads, lds, st>>>(in, cin, wk, bias, cout, 64, out, acc);
-        return SPAI_OK;
+#ifdef SPAI_SLICE_NT2   // variant: 32-channel slices, the K split over 2 wave pairs
+    if constexpr (ks % 2 == 0) {
+        if (nt % 2 == 0) {
+            k_conv_mfma<CINP, 2><<<dim3(B, nt / 2), kThreads, lds, st>>>(in, cin, wk, bias, cout, 16 * nt, out, acc);
+            return SPAI_OK;
+        }
     }
 #endif
-#ifndef SPAI_SLICE_MIN_CINP
-#define SPAI_SLICE_MIN_CINP 32
-#endif
-    if constexpr (ks % 4 == 0 && CINP >= SPAI_SLICE_MIN_CINP) {
+    if constexpr (ks % 4 == 0) {
         k_conv_mfma<CINP, 1><<<dim3(B, nt), kThreads, lds, st>>>(in, cin, wk, bias, cout, 16 * nt, out, acc);
         return SPAI_OK;
     }
