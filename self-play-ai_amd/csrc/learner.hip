@@ -454,17 +454,6 @@ __global__ __launch_bounds__(kBn) void k_bn_bwd(const float *__restrict__ da, co
 }
 
 // ------------------------------------------------------------------ heads + loss
-__device__ __forceinline__ float block_sum(float v, float *red) {
-    red[threadIdx.x] = v;
-    __syncthreads();
-    for (int s = kThreads / 2; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-        __syncthreads();
-    }
-    const float r = red[0];
-    __syncthreads();
-    return r;
-}
 
 // one workgroup per sample: policy logits (1344 -> 7), value (126 -> 1, tanh),
 // loss terms and the output gradients
@@ -475,18 +464,31 @@ __global__ __launch_bounds__(kThreads) void k_heads_loss(const float *__restrict
                                                          const float *__restrict__ pi, const float *__restrict__ zv,
                                                          int B, float *__restrict__ dlogits, float *__restrict__ dpre,
                                                          float *__restrict__ loss_terms) {
-    __shared__ float red[kThreads];
-    const int b = blockIdx.x;
+    __shared__ float part[kThreads / 64][8];
+    const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const float *xp = rp + (size_t)b * 32 * kCells, *xv = rv + (size_t)b * 3 * kCells;
-    float lg[7];
-    for (int o = 0; o < 7; ++o) {
-        float s = 0.f;
-        for (int k = threadIdx.x; k < 32 * kCells; k += kThreads) s += xp[k] * wp[o * 32 * kCells + k];
-        lg[o] = block_sum(s, red) + bp[o];
+    // one pass over the features: 7 policy logits and the value pre-activation at
+    // once; wave sums by shuffles, then the 4 wave partials in order
+    float acc8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int k = threadIdx.x; k < 32 * kCells; k += kThreads) {
+        const float xk = xp[k];
+#pragma unroll
+        for (int o = 0; o < 7; ++o) acc8[o] += xk * wp[o * 32 * kCells + k];
     }
-    float s = 0.f;
-    for (int k = threadIdx.x; k < 3 * kCells; k += kThreads) s += xv[k] * wv[k];
-    const float pre = block_sum(s, red) + bv[0];
+    for (int k = threadIdx.x; k < 3 * kCells; k += kThreads) acc8[7] += xv[k] * wv[k];
+#pragma unroll
+    for (int o = 0; o < 8; ++o) {
+#pragma unroll
+        for (int sh = 32; sh > 0; sh >>= 1) acc8[o] += __shfl_xor(acc8[o], sh, 64);
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int o = 0; o < 8; ++o) part[wave][o] = acc8[o];
+    __syncthreads();
+    float lg[7];
+#pragma unroll
+    for (int o = 0; o < 7; ++o) lg[o] = ((part[0][o] + part[1][o]) + part[2][o]) + part[3][o] + bp[o];
+    const float pre = ((part[0][7] + part[1][7]) + part[2][7]) + part[3][7] + bv[0];
     if (threadIdx.x == 0) {
         float mx = lg[0];
         for (int o = 1; o < 7; ++o) mx = fmaxf(mx, lg[o]);
@@ -533,9 +535,15 @@ __global__ __launch_bounds__(kThreads) void k_linear_bwd_w(const float *__restri
     part[q][lane] = s;
     __syncthreads();
     if (q == 0 && i < O * K) dw[i] = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
-    if (blockIdx.x == 0 && q == 1 && lane < O) {
+    if (blockIdx.x == 0 && q == 1 && lane < O) {   // db: 16 loads in flight, summed in batch order
         float t = 0.f;
-        for (int b = 0; b < B; ++b) t += dy[b * O + lane];
+        for (int b0 = 0; b0 < B; b0 += 16) {
+            float v[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v[j] = b0 + j < B ? dy[(b0 + j) * O + lane] : 0.f;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) t += v[j];
+        }
         db[lane] = t;
     }
 }
