@@ -842,7 +842,9 @@ void learner_destroy(spai_learner *L) {
 int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in, const float *pi_in,
                  const float *z_in, const float *bc) {
     float *P = L->p.p, *G = L->g.p;
-    SPAI_HIP(hipMemsetAsync(G, 0, L->n_params * 4, st));
+    // G needs no clearing: every trainable entry is written (not accumulated) by
+    // this step's kernels, and the BN running-statistic entries stay at the zero
+    // they got at learner_create
     const float eps = L->cfg.bn_eps, mom = L->cfg.bn_momentum;
     const size_t nl = L->convs.size();
     k_pack_all<<<dim3(blocks_of((size_t)9 * 64 * 64), L->n_pack), kThreads, 0, st>>>(P, L->pack_desc.p, L->wt.p);
