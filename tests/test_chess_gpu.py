@@ -224,6 +224,24 @@ def test_chess_net_positions_per_workgroup_invariance(ch, sc):
     eng.close()
 
 
+def test_chess_net_work_split_invariance(ch, sc):
+    """more positions than CUs: m = ceil(count / #CUs) positions on the busiest
+    CU; even m runs P = 2 passes, odd m an even split as P = 2 passes plus one
+    P = 1 pass (k_chess_forward).  Every count must give the one-position-per-
+    workgroup results bit for bit."""
+    rng = np.random.default_rng(5)
+    x = (rng.random((1300, 19, 8, 8)) < 0.2).astype(np.float32)
+    eng = sc.ChessEngine(num_searches=4, max_trees=8)
+    net = sc.ChessNet(eng, 2, sc.init_params(2, 3))
+    ref_l, ref_v = zip(*(net.forward(x[i:i + 200]) for i in range(0, 1300, 200)))   # <= #CUs: P = 1
+    ref_l, ref_v = np.concatenate(ref_l), np.concatenate(ref_v)
+    for n in (600, 700, 1000, 1100, 1300):   # m = 3, 3, 4, 5, 6 on 256 CUs
+        lg, v = net.forward(x[:n])
+        assert np.array_equal(lg, ref_l[:n]) and np.array_equal(v, ref_v[:n]), n
+    net.close()
+    eng.close()
+
+
 def test_chess_net_20_blocks_vs_fp64(ch, sc):
     rng = random.Random(9)
     xs = []
