@@ -35,7 +35,10 @@ namespace spai {
 namespace {
 
 constexpr int kLanesPerTree = 8;
-constexpr int kBlock = 256;
+#ifndef SPAI_TREE_BLOCK
+#define SPAI_TREE_BLOCK 256
+#endif
+constexpr int kBlock = SPAI_TREE_BLOCK;   // threads per tree-kernel workgroup (kBlock / 8 trees)
 constexpr int kTreesPerBlock = kBlock / kLanesPerTree;
 constexpr uint32_t kErrNan = 1u, kErrCapacity = 2u, kErrDepth = 4u;
 
