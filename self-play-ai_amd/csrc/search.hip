@@ -36,7 +36,7 @@ namespace {
 
 constexpr int kLanesPerTree = 8;
 #ifndef SPAI_TREE_BLOCK
-#define SPAI_TREE_BLOCK 256
+#define SPAI_TREE_BLOCK 64
 #endif
 constexpr int kBlock = SPAI_TREE_BLOCK;   // threads per tree-kernel workgroup (kBlock / 8 trees)
 constexpr int kTreesPerBlock = kBlock / kLanesPerTree;
