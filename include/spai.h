@@ -258,6 +258,10 @@ int spai_learner_train(spai_learner *l, uint32_t n, const float *states, const f
  * (after the cross-rank reduction, before the 1/world scale), flat order */
 int spai_learner_params(spai_learner *l, float *params, size_t n_params);
 int spai_learner_grads(spai_learner *l, float *grads, size_t n_params);
+/* the last train step's post-ReLU activations of conv layer `layer` (stem, the
+ * 2*blocks residual convs, policy head, value head), [B][co][6][7]: the ReLU
+ * masks the step took, for checking gradients against a float64 restatement */
+int spai_learner_activation(spai_learner *l, int layer, float *out, size_t n);
 /* RCCL communicator for a data-parallel learner: rank 0 makes the id
  * (spai_comm_unique_id), the host side broadcasts it, every rank joins.
  * world 1 with an id builds a 1-rank communicator (the all-reduce is then a
@@ -305,7 +309,28 @@ int spai_choose_multiple(uint32_t n, uint32_t k, uint64_t seed, uint64_t stream,
  * checkpoint_dir is set, saves {checkpoint_dir}/{iter}.safetensors.
  * Reference defaults (SelfPlayArgs / TrainingArgs / C4 Args): c 2, 600 sims,
  * T 1.25, 100 games, batch 128, 20 batches x 10 iters, capacity 12800,
- * fraction 0.3, 4 blocks. */
+ * fraction 0.3, 4 blocks.
+ *
+ * Optional observer (cfg.observer, NULL = none): called under the replay ring's
+ * lock, so the events arrive in ring order.  A PUSH event carries a worker's
+ * subsample (n = (positions as f32 * fraction) as usize, learner_concurrent.rs:278)
+ * and the weight version its games were played with; a POP event carries the
+ * batch the trainer took for one train step and the number of weight versions
+ * published so far.  Tests replay the events through a HeapRb model.  The
+ * callback must not call back into the pipeline. */
+enum { SPAI_PIPE_PUSH = 0, SPAI_PIPE_POP = 1 };
+typedef struct spai_pipeline_event {
+    int32_t kind;          /* SPAI_PIPE_PUSH / SPAI_PIPE_POP */
+    uint32_t worker;       /* push: worker index; pop: 0 */
+    uint64_t batch;        /* push: the worker's self-play batch number; pop: train step */
+    uint64_t version;      /* push: weight version played with; pop: versions published */
+    uint32_t n;            /* samples pushed / popped */
+    uint32_t positions;    /* push: positions of the self-play batch; pop: 0 */
+    uint32_t ring_size;    /* samples buffered after the event */
+    uint32_t pad;
+    const float *states, *policies, *values;   /* [n][126], [n][7], [n] */
+} spai_pipeline_event;
+typedef void (*spai_pipeline_observer)(void *user, const spai_pipeline_event *ev);
 typedef struct spai_pipeline_config {
     uint32_t n_selfplay;
     const int *selfplay_devices;   /* [n_selfplay] */
@@ -317,6 +342,8 @@ typedef struct spai_pipeline_config {
     int blocks;
     uint64_t seed;
     const char *checkpoint_dir;    /* NULL: no checkpoints */
+    spai_pipeline_observer observer;   /* NULL: no events */
+    void *observer_user;
 } spai_pipeline_config;
 typedef struct spai_pipeline_stats {
     double games, positions, samples_pushed, samples_overwritten, batches_trained;
@@ -361,8 +388,9 @@ typedef struct spai_chess_state {
 typedef struct spai_chess spai_chess;
 typedef struct spai_chess_net spai_chess_net;
 
-/* cfg.max_moves = longest game (sizes the transposition tables).  Default 11,904: the
- * fifty-move rule bounds a game at 11,898 plies, so the default never overflows. */
+/* cfg.max_moves = longest game (sizes the transposition tables).  Default 12,304: the
+ * fifty-move counter (reset by pawn moves, captures and at most 4 castle-rights
+ * changes) bounds a game at 12,298 plies, so the default covers every legal game. */
 int spai_chess_config_default(spai_config *cfg);
 int spai_chess_create(const spai_config *cfg, int device, spai_chess **out);
 int spai_chess_destroy(spai_chess *e);
@@ -387,6 +415,12 @@ int spai_chess_encode(spai_chess *e, uint32_t first, uint32_t n, float *out);
  * over slots [first, first+n): ms[0] legal move lists + counts + status,
  * ms[1] encoding.  Measurement only; slots are not modified. */
 int spai_chess_rules_bench(spai_chess *e, uint32_t first, uint32_t n, uint32_t iters, double *ms);
+/* perft of slot `slot`'s position on the device: counts[d-1] = the number of legal
+ * move sequences of length d, d = 1..depth (<= 8), by the movegen and make-move
+ * the search uses (MoveGen::new_legal / Board::make_move of the chess crate,
+ * game/chess.rs:54,117-118); breadth first, one Board array per ply in HBM
+ * (SPAI_ERR_CAPACITY past 2^26 positions in one ply) */
+int spai_chess_perft(spai_chess *e, uint32_t slot, int depth, uint64_t *counts);
 /* mask_invalid_actions (chess.rs:252-275): policy [n][len] -> out [n][4672]; len must be 4672 */
 int spai_chess_mask_invalid(spai_chess *e, uint32_t first, uint32_t n, const float *policy, uint32_t len,
                             float *out);

@@ -75,8 +75,13 @@ def _col2im(dcols, B, C):
 
 
 def train_step(params, adam_m, adam_v, step, x, pi, z, blocks, hidden, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8,
-               momentum=0.1, bn_eps=1e-5):
-    """one optimizer step; returns (new params, m, v, loss[3], grads) — all float64"""
+               momentum=0.1, bn_eps=1e-5, masks=None, diag=None):
+    """one optimizer step; returns (new params, m, v, loss[3], grads) — all float64.
+
+    masks: optional per-conv-layer boolean [B][co][6][7] ReLU masks to use instead of
+    (pre-activation > 0) — e.g. the device step's own (post-ReLU activation > 0), so
+    that a pre-activation within rounding of 0 takes the same side of the kink in
+    both.  diag: optional dict that receives the pre-activations ("pre", per layer)."""
     convs, lin, n = _layout(blocks, hidden)
     P = np.asarray(params, np.float64).copy()
     G = np.zeros(n)
@@ -100,8 +105,11 @@ def train_step(params, adam_m, adam_v, step, x, pi, z, blocks, hidden, lr=1e-3, 
         y = P[c["g"]:c["g"] + co][None, :, None, None] * xhat + P[c["be"]:c["be"] + co][None, :, None, None]
         if res is not None:
             y = y + res
-        a = np.maximum(y, 0.0)
-        cache[l] = dict(cols=cols, W=W, xhat=xhat, inv=inv, a=a, inp_shape=inp.shape)
+        mask = (y > 0.0) if masks is None else np.asarray(masks[l], bool).reshape(y.shape)
+        a = np.where(mask, y, 0.0)
+        if diag is not None:
+            diag.setdefault("pre", [None] * len(convs))[l] = y
+        cache[l] = dict(cols=cols, W=W, xhat=xhat, inv=inv, a=a, m=mask, inp_shape=inp.shape)
         return a
 
     cache = [None] * len(convs)
@@ -134,7 +142,7 @@ def train_step(params, adam_m, adam_v, step, x, pi, z, blocks, hidden, lr=1e-3, 
     def bn_conv_bwd(l, da, want_dx=True):
         c, cc = convs[l], cache[l]
         co, ci = c["co"], c["ci"]
-        dy = da * (cc["a"] > 0)
+        dy = da * cc["m"]
         xhat, inv = cc["xhat"], cc["inv"]
         nn_ = B * CELLS
         sb = dy.sum((0, 2, 3))
@@ -154,7 +162,7 @@ def train_step(params, adam_m, adam_v, step, x, pi, z, blocks, hidden, lr=1e-3, 
     dh = dh + bn_conv_bwd(nval, (dpre[:, None] @ Wv).reshape(B, 3, ROWS, COLS))
     for k in reversed(range(blocks)):
         l1, l2 = 1 + 2 * k, 2 + 2 * k
-        dt = dh * (cache[l2]["a"] > 0)
+        dt = dh * cache[l2]["m"]
         dr1 = bn_conv_bwd(l2, dt)
         dh = dt + bn_conv_bwd(l1, dr1)
     bn_conv_bwd(0, dh, want_dx=False)

@@ -36,7 +36,10 @@ def main():
                            train_iters=a.iters, replay_capacity=a.capacity, blocks=a.blocks, seed=a.seed)
     st.update(selfplay_devices=list(devs), learner_device=a.learner_device, games_per_batch=a.games, sims=a.sims,
               batch=a.batch, blocks=a.blocks, games_per_sec=st["games"] / st["seconds"],
-              trained_samples_per_sec=st["batches_trained"] * a.batch / st["seconds"])
+              trained_samples_per_sec=st["batches_trained"] * a.batch / st["seconds"],
+              # every live tree searches every move: sims = positions x sims per move
+              selfplay_sims_per_sec=st["positions"] * a.sims / st["seconds"],
+              workers=len(devs))
     print(json.dumps(st), flush=True)
 
 

@@ -444,6 +444,13 @@ int spai_learner_grads(spai_learner *l, float *grads, size_t n) {
     return learner_params(l, grads, n, true);
 }
 
+int spai_learner_activation(spai_learner *l, int layer, float *out, size_t n) {
+    PTR_CHECK(l);
+    PTR_CHECK(out);
+    ENG_CHECK(l->eng);
+    return learner_activation(l, layer, out, n);
+}
+
 int spai_comm_unique_id(uint8_t *id) {
     PTR_CHECK(id);
     return comm_unique_id(id);

@@ -86,9 +86,13 @@ int spai_chess_config_default(spai_config *cfg) {
     cfg->max_trees = 1024;      // BASELINE config 4 (1024 parallel games)
     // longest game: transposition-table entries per game.  The reference's rules end a
     // game by the fifty-move counter (chess.rs:124-144,154-166: a draw at 100 plies with
-    // no pawn move, capture or castle-right change), which bounds any game at 5,949
-    // moves = 11,898 plies; 11,904 entries (93 KB per game) can therefore never overflow.
-    cfg->max_moves = 11904;
+    // no pawn move, capture or castle-right change).  Pawn moves and captures alone bound
+    // a game at 5,949 moves = 11,898 plies; the reference's extra reset on a castle-rights
+    // change can happen at most 4 more times (each side loses its kingside and queenside
+    // rights separately), each worth at most 100 further plies: 12,298 plies.  12,304
+    // entries (96 KB per game) therefore cover the longest legal game; a longer one would
+    // be reported as SPAI_ERR_CAPACITY ("game longer than cfg.max_moves").
+    cfg->max_moves = 12304;
     cfg->eval = SPAI_EVAL_NET;
     cfg->seed = 0;
     return SPAI_OK;
@@ -175,6 +179,12 @@ int spai_chess_rules_bench(spai_chess *e, uint32_t first, uint32_t n, uint32_t i
     CH_CHECK(e);
     CH_PTR(ms);
     return slots_rules_bench(e, first, n, iters, ms);
+}
+
+int spai_chess_perft(spai_chess *e, uint32_t slot, int depth, uint64_t *counts) {
+    CH_CHECK(e);
+    CH_PTR(counts);
+    return perft(e, slot, depth, counts);
 }
 
 int spai_chess_encode(spai_chess *e, uint32_t first, uint32_t n, float *out) {

@@ -110,6 +110,7 @@ int slots_status(spai_chess *e, uint32_t first, uint32_t n, uint8_t *status, uin
 int slots_encode(spai_chess *e, uint32_t first, uint32_t n, float *out);
 int slots_mask(spai_chess *e, uint32_t first, uint32_t n, const float *policy, uint32_t len, float *out);
 int slots_rules_bench(spai_chess *e, uint32_t first, uint32_t n, uint32_t iters, double *ms);
+int perft(spai_chess *e, uint32_t slot, int depth, uint64_t *counts);
 // device-pointer forms used by net_predict (chess_net.hip)
 int slots_encode_device(spai_chess *e, uint32_t first, uint32_t n, float *d_out);   // f32 [n][19][64]
 int slots_softmax_mask_device(spai_chess *e, uint32_t first, uint32_t n, const float *d_logits, float *d_out);

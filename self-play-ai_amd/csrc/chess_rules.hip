@@ -446,6 +446,93 @@ int slots_rules_bench(spai_chess *e, uint32_t first, uint32_t n, uint32_t iters,
     return rc;
 }
 
+// ---------------------------------------------------------------- perft
+// Breadth-first perft on the device: the positions of one ply live in a flat
+// Board array; each wave generates one position's legal moves (wave_movegen,
+// the same routine as search and self-play) and either counts them or writes
+// the children (apply_move) at slots taken by one atomic per wave.  Pins the
+// device move generator to the public perft counts (the crate's MoveGen::new_legal
+// + Board::make_move, game/chess.rs:54,117-118).
+__global__ void k_perft_count(const Board *__restrict__ level, uint64_t n, unsigned long long *__restrict__ total) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const Board b = level[i];
+    const GenOut g = wave_movegen(b, lane, [](int, int) {});
+    if (lane == 0 && g.n) atomicAdd(total, (unsigned long long)g.n);
+}
+
+__global__ void k_perft_expand(const Board *__restrict__ level, uint64_t n, Board *__restrict__ next, uint64_t cap,
+                               unsigned long long *__restrict__ fill) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t i = (uint64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (i >= n) return;
+    const Board b = level[i];
+    const GenOut g = wave_movegen(b, lane, [](int, int) {});
+    unsigned long long base = 0;
+    if (lane == 0 && g.n) base = atomicAdd(fill, (unsigned long long)g.n);
+    base = __shfl(base, 0, 64);
+    wave_movegen(b, lane, [&](int off, int mv) {
+        if (base + off < cap) {
+            Board c = b;
+            apply_move(c, mv);
+            next[base + off] = c;
+        }
+    });
+}
+
+struct PerftBufs {   // DevBuf has no destructor: free the ply buffers on every exit
+    DevBuf<Board> cur, nxt;
+    DevBuf<unsigned long long> ctr;
+    ~PerftBufs() {
+        cur.release();
+        nxt.release();
+        ctr.release();
+    }
+};
+
+// counts[d - 1] = perft(d) of slot `slot`'s position for d = 1..depth
+int perft(spai_chess *e, uint32_t slot, int depth, uint64_t *counts) {
+    SPAI_CHECK(slot < e->slots.n, SPAI_ERR_INVALID, "slot %u out of range (%u)", slot, e->slots.n);
+    SPAI_CHECK(depth >= 1 && depth <= 8, SPAI_ERR_INVALID, "perft depth %d not in 1..8", depth);
+    constexpr uint64_t kMaxLevel = 1ull << 26;   // 4.8 GB of boards per ply
+    PerftBufs B;
+    DevBuf<Board> &cur = B.cur, &nxt = B.nxt;
+    DevBuf<unsigned long long> &ctr = B.ctr;
+    SPAI_TRY(cur.alloc(1));
+    SPAI_TRY(ctr.alloc(2));
+    hipStream_t st = e->stream;
+    SPAI_HIP(hipMemcpyAsync(cur.p, e->slots.board.p + slot, sizeof(Board), hipMemcpyDeviceToDevice, st));
+    uint64_t n = 1;
+    for (int d = 1; d <= depth; ++d) {
+        unsigned long long h[2] = {0, 0};
+        SPAI_HIP(hipMemsetAsync(ctr.p, 0, sizeof(h), st));
+        const unsigned grid = (unsigned)((n + kWavesPerBlock - 1) / kWavesPerBlock);
+        k_perft_count<<<grid, 64 * kWavesPerBlock, 0, st>>>(cur.p, n, ctr.p);
+        SPAI_HIP(hipGetLastError());
+        SPAI_HIP(hipMemcpyAsync(h, ctr.p, sizeof(h), hipMemcpyDeviceToHost, st));
+        SPAI_HIP(hipStreamSynchronize(st));
+        counts[d - 1] = h[0];
+        if (d == depth || h[0] == 0) {
+            for (int k = d; k < depth; ++k) counts[k] = 0;
+            break;
+        }
+        SPAI_CHECK(h[0] <= kMaxLevel, SPAI_ERR_CAPACITY, "perft: ply %d holds %llu positions (limit %llu)", d,
+                   (unsigned long long)h[0], (unsigned long long)kMaxLevel);
+        SPAI_TRY(nxt.alloc(h[0]));
+        k_perft_expand<<<grid, 64 * kWavesPerBlock, 0, st>>>(cur.p, n, nxt.p, h[0], ctr.p + 1);
+        SPAI_HIP(hipGetLastError());
+        SPAI_HIP(hipMemcpyAsync(&h[1], ctr.p + 1, sizeof(h[1]), hipMemcpyDeviceToHost, st));
+        SPAI_HIP(hipStreamSynchronize(st));
+        SPAI_CHECK(h[1] == h[0], SPAI_ERR_DEVICE, "perft: ply %d expanded %llu of %llu children", d,
+                   (unsigned long long)h[1], (unsigned long long)h[0]);
+        std::swap(cur, nxt);
+        nxt.release();
+        n = h[0];
+    }
+    return SPAI_OK;
+}
+
 int slots_encode_device(spai_chess *e, uint32_t first, uint32_t n, float *d_out) {
     RANGE_CHECK(e, first, n);
     if (!n) return SPAI_OK;

@@ -985,6 +985,7 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
     // (a hipGraph of this step, captured once per batch size, measured 130k
     // samples/s against 162k eager: profiles/r02/learner/graph_ab.txt)
     SPAI_TRY(enqueue_step(L, B, st, x_in, pi_in, z_in, bc));
+    L->last_batch = B;
     float *terms = L->stage + nin + 2;   // the staged inputs were consumed by the DMA above (stream order)
     SPAI_HIP(hipMemcpyAsync(terms, L->loss_terms.p, (size_t)B * 2 * 4, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipStreamSynchronize(st));
@@ -1034,6 +1035,20 @@ int learner_params(spai_learner *L, float *params, size_t n, bool grads) {
     SPAI_CHECK(n == L->n_params, SPAI_ERR_INVALID, "expected %zu params, got %zu", L->n_params, n);
     hipStream_t st = L->eng->stream;
     SPAI_HIP(hipMemcpyAsync(params, grads ? L->g.p : L->p.p, n * 4, hipMemcpyDeviceToHost, st));
+    SPAI_HIP(hipStreamSynchronize(st));
+    return SPAI_OK;
+}
+
+// the latest step's post-ReLU activations of conv layer `layer` (construction
+// order: stem, 2*blocks residual convs, policy head, value head), [B][co][6][7]
+int learner_activation(spai_learner *L, int layer, float *out, size_t n) {
+    SPAI_CHECK(layer >= 0 && (size_t)layer < L->convs.size(), SPAI_ERR_INVALID, "layer %d of %zu", layer,
+               L->convs.size());
+    SPAI_CHECK(L->last_batch > 0, SPAI_ERR_INVALID, "no train step yet");
+    const size_t want = (size_t)L->last_batch * L->convs[layer].co * kCells;
+    SPAI_CHECK(n == want, SPAI_ERR_INVALID, "expected %zu activations, got %zu", want, n);
+    hipStream_t st = L->eng->stream;
+    SPAI_HIP(hipMemcpyAsync(out, L->a[layer].p, n * 4, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipStreamSynchronize(st));
     return SPAI_OK;
 }

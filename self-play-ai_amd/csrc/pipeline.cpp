@@ -58,8 +58,11 @@ int replay_create(uint32_t capacity, spai_replay **out) {
 
 void replay_destroy(spai_replay *r) { delete r; }
 
-// push_iter_overwrite: append in order; when full, the oldest sample is dropped
-int replay_push(spai_replay *r, uint32_t n, const float *s, const float *p, const float *v) {
+// push_iter_overwrite: append in order; when full, the oldest sample is dropped.
+// `ev` (optional) is completed with the ring size and handed to the observer
+// while the lock is held, so observers see pushes and pops in ring order.
+int replay_push(spai_replay *r, uint32_t n, const float *s, const float *p, const float *v,
+                const Observer *obs) {
     {
         std::lock_guard<std::mutex> lk(r->mu);
         for (uint32_t i = 0; i < n; ++i) {
@@ -75,6 +78,16 @@ int replay_push(spai_replay *r, uint32_t n, const float *s, const float *p, cons
             r->size += 1;
         }
         r->pushed += n;
+        if (obs && obs->fn) {
+            spai_pipeline_event ev = obs->ev;
+            ev.kind = SPAI_PIPE_PUSH;
+            ev.n = n;
+            ev.ring_size = r->size;
+            ev.states = s;
+            ev.policies = p;
+            ev.values = v;
+            obs->fn(obs->user, &ev);
+        }
     }
     r->cv.notify_all();
     return SPAI_OK;
@@ -83,7 +96,7 @@ int replay_push(spai_replay *r, uint32_t n, const float *s, const float *p, cons
 // pop_iter().take(n) from the oldest end; wait_ms < 0 blocks until n are buffered
 // (or `stop` is set), 0 fails at once when fewer are there
 int replay_pop(spai_replay *r, uint32_t n, float *s, float *p, float *v, int wait_ms,
-               const std::atomic<bool> *stop = nullptr) {
+               const std::atomic<bool> *stop = nullptr, const Observer *obs = nullptr) {
     std::unique_lock<std::mutex> lk(r->mu);
     SPAI_CHECK(n <= r->capacity, SPAI_ERR_INVALID, "pop of %u from a ring of %u", n, r->capacity);
     auto ready = [&] { return r->size >= n || (stop && stop->load()); };
@@ -99,6 +112,16 @@ int replay_pop(spai_replay *r, uint32_t n, float *s, float *p, float *v, int wai
     r->head = (r->head + n) % r->capacity;
     r->size -= n;
     r->popped += n;
+    if (obs && obs->fn) {
+        spai_pipeline_event ev = obs->ev;
+        ev.kind = SPAI_PIPE_POP;
+        ev.n = n;
+        ev.ring_size = r->size;
+        ev.states = s;
+        ev.policies = p;
+        ev.values = v;
+        obs->fn(obs->user, &ev);
+    }
     return SPAI_OK;
 }
 
@@ -214,7 +237,12 @@ int pipeline_run(const spai_pipeline_config *cfg, const float *init_params, size
                 memcpy(&p[(size_t)i * kPol], &col.p[(size_t)pick[i] * kPol], kPol * 4);
                 v[i] = col.v[pick[i]];
             }
-            replay_push(ring, k, s.data(), p.data(), v.data());
+            Observer ob{cfg->observer, cfg->observer_user, spai_pipeline_event{}};
+            ob.ev.worker = w;
+            ob.ev.batch = batch;
+            ob.ev.version = ver;
+            ob.ev.positions = n;
+            replay_push(ring, k, s.data(), p.data(), v.data(), &ob);
             games += cfg->games_per_batch;
             positions += n;
         }
@@ -249,7 +277,13 @@ int pipeline_run(const spai_pipeline_config *cfg, const float *init_params, size
     std::vector<float> bs((size_t)B * kEnc), bp((size_t)B * kPol), bv(B), params(n_params);
     for (uint32_t it = 0; rc == SPAI_OK && it < cfg->train_iters; ++it) {
         for (uint32_t k = 0; rc == SPAI_OK && k < cfg->batches_per_iter; ++k) {
-            rc = replay_pop(ring, B, bs.data(), bp.data(), bv.data(), -1, &aborted);
+            Observer ob{cfg->observer, cfg->observer_user, spai_pipeline_event{}};
+            ob.ev.batch = (uint64_t)batches;
+            {
+                std::lock_guard<std::mutex> lk(pub.mu);
+                ob.ev.version = pub.version;
+            }
+            rc = replay_pop(ring, B, bs.data(), bp.data(), bv.data(), -1, &aborted, &ob);
             if (rc != SPAI_OK) break;   // only when the workers failed
             float loss[3];
             rc = spai_learner_train_batch(L, B, bs.data(), bp.data(), bv.data(), loss);

@@ -474,8 +474,11 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
     }
     for (int h = 0; h < nchain; ++h) {   // per-iteration leaf counters (also the batch slot counters)
         Batch &B = e->batch[h];
-        if (B.iter_counts.n < num_searches) SPAI_TRY(B.iter_counts.alloc(std::max<uint32_t>(num_searches, 1)));
-        SPAI_HIP(hipMemsetAsync(B.iter_counts.p, 0, (size_t)std::max<uint32_t>(num_searches, 1) * 4, st));
+        // at least one counter even for num_searches == 0, so the memset never sees a
+        // null buffer on a fresh engine
+        const uint32_t nc = std::max<uint32_t>(num_searches, 1);
+        if (B.iter_counts.n < nc) SPAI_TRY(B.iter_counts.alloc(nc));
+        SPAI_HIP(hipMemsetAsync(B.iter_counts.p, 0, (size_t)nc * 4, st));
     }
     SPAI_HIP(hipMemcpyAsync(e->active.p, tree_idx, n * 4, hipMemcpyHostToDevice, st));
     SPAI_HIP(hipMemsetAsync(e->err.p, 0, 4, st));

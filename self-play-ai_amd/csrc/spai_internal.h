@@ -136,6 +136,7 @@ struct spai_learner {
     spai_adam_config cfg{};
     uint64_t step = 0;
     uint32_t max_batch = 0;
+    uint32_t last_batch = 0;            // B of the latest train step (its activations stay in `a`)
     size_t n_params = 0;
     struct Conv {
         int ci, co;
@@ -231,6 +232,7 @@ int learner_create(spai_engine *e, int blocks, int hidden, const float *params, 
 void learner_destroy(spai_learner *l);
 int learner_train_batch(spai_learner *l, uint32_t n, const float *states, const float *policies, const float *values,
                         float *loss3);
+int learner_activation(spai_learner *L, int layer, float *out, size_t n);
 int learner_params(spai_learner *l, float *params, size_t n, bool grads);
 int learner_train_epochs(spai_learner *l, uint32_t n, const float *states, const float *policies, const float *values,
                          uint32_t epochs, uint32_t batch, uint64_t seed, float *loss3);
@@ -245,7 +247,13 @@ int params_load_safetensors(int game, int blocks, int hidden, const char *path, 
 // pipeline.cpp
 int replay_create(uint32_t capacity, spai_replay **out);
 void replay_destroy(spai_replay *r);
-int replay_push(spai_replay *r, uint32_t n, const float *s, const float *p, const float *v);
+struct Observer {   // pipeline event hook (spai_pipeline_config::observer) and the event's fixed fields
+    spai_pipeline_observer fn;
+    void *user;
+    spai_pipeline_event ev;
+};
+int replay_push(spai_replay *r, uint32_t n, const float *s, const float *p, const float *v,
+                const Observer *obs = nullptr);
 int replay_pop_now(spai_replay *r, uint32_t n, float *s, float *p, float *v);
 int replay_size(spai_replay *r, uint32_t *n);
 void choose_multiple(uint32_t n, uint32_t k, uint64_t seed, uint64_t stream, std::vector<uint32_t> &out);

@@ -34,7 +34,7 @@ SYMBOLS = [
     "spai_tree_reset", "spai_search", "spai_tree_use_subtree", "spai_tree_node", "spai_tree_size",
     "spai_selfplay_run", "spai_engine_set_timing", "spai_engine_timing", "spai_engine_timing_items",
     "spai_net_phase_cycles", "spai_net_bench", "spai_adam_config_default", "spai_learner_create", "spai_learner_destroy",
-    "spai_learner_train_batch", "spai_learner_params", "spai_learner_grads", "spai_comm_unique_id",
+    "spai_learner_train_batch", "spai_learner_params", "spai_learner_grads", "spai_learner_activation", "spai_comm_unique_id",
     "spai_learner_set_comm", "spai_learner_broadcast", "spai_params_save_safetensors", "spai_params_load_safetensors",
     "spai_replay_create", "spai_replay_destroy", "spai_replay_push", "spai_replay_pop", "spai_replay_size",
     "spai_choose_multiple", "spai_pipeline_config_default", "spai_pipeline_run", "spai_learner_train",
@@ -42,7 +42,7 @@ SYMBOLS = [
     # chess (spai_chess.py)
     "spai_chess_config_default", "spai_chess_create", "spai_chess_destroy", "spai_chess_sync",
     "spai_chess_games_resize", "spai_chess_games_write", "spai_chess_games_read", "spai_chess_legal_moves",
-    "spai_chess_apply", "spai_chess_status", "spai_chess_encode", "spai_chess_rules_bench", "spai_chess_mask_invalid",
+    "spai_chess_apply", "spai_chess_status", "spai_chess_encode", "spai_chess_rules_bench", "spai_chess_perft", "spai_chess_mask_invalid",
     "spai_chess_move_index", "spai_chess_index_move", "spai_chess_net_num_params", "spai_chess_net_init_params",
     "spai_chess_net_create", "spai_chess_net_destroy", "spai_chess_net_forward", "spai_chess_predict", "spai_chess_set_net",
     "spai_chess_trees_create", "spai_chess_search", "spai_chess_tree_reset", "spai_chess_tree_use_subtree", "spai_chess_tree_root", "spai_chess_trees_advance",
@@ -87,7 +87,19 @@ class PipelineConfig(C.Structure):
                 ("games_per_batch", C.c_uint32), ("num_searches", C.c_uint32), ("c", C.c_float),
                 ("temperature", C.c_float), ("batch_size", C.c_uint32), ("batches_per_iter", C.c_uint32),
                 ("train_iters", C.c_uint32), ("replay_capacity", C.c_uint32), ("sample_fraction", C.c_float),
-                ("blocks", C.c_int), ("seed", C.c_uint64), ("checkpoint_dir", C.c_char_p)]
+                ("blocks", C.c_int), ("seed", C.c_uint64), ("checkpoint_dir", C.c_char_p),
+                ("observer", C.c_void_p), ("observer_user", C.c_void_p)]
+
+
+class PipelineEvent(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("worker", C.c_uint32), ("batch", C.c_uint64), ("version", C.c_uint64),
+                ("n", C.c_uint32), ("positions", C.c_uint32), ("ring_size", C.c_uint32), ("pad", C.c_uint32),
+                ("states", C.POINTER(C.c_float)), ("policies", C.POINTER(C.c_float)),
+                ("values", C.POINTER(C.c_float))]
+
+
+PIPE_PUSH, PIPE_POP = 0, 1
+OBSERVER = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(PipelineEvent))
 
 
 class PipelineStats(C.Structure):
@@ -157,6 +169,7 @@ def lib():
         L.spai_learner_train_batch.argtypes = [vp, u32, vp, vp, vp, vp]
         L.spai_learner_params.argtypes = [vp, vp, C.c_size_t]
         L.spai_learner_grads.argtypes = [vp, vp, C.c_size_t]
+        L.spai_learner_activation.argtypes = [vp, C.c_int, vp, C.c_size_t]
         L.spai_learner_train.argtypes = [vp, u32, vp, vp, vp, u32, u32, u64, vp]
         L.spai_comm_unique_id.argtypes = [vp]
         L.spai_learner_set_comm.argtypes = [vp, i32, i32, vp]
@@ -426,6 +439,8 @@ class Learner:
             setattr(cfg, k, float(v))
         self.params0 = np.ascontiguousarray(params, np.float32)
         self.n = len(self.params0)
+        self.blocks, self.hidden = blocks, hidden
+        self.last_batch = 0
         self.h = C.c_void_p()
         _check(lib().spai_learner_create(engine.h, blocks, hidden, _p(self.params0), self.n, C.byref(cfg),
                                          C.byref(self.h)))
@@ -437,6 +452,7 @@ class Learner:
         assert len(x) == len(pi) == len(z)
         loss = np.zeros(3, np.float32)
         _check(lib().spai_learner_train_batch(self.h, len(x), _p(x), _p(pi), _p(z), _p(loss)))
+        self.last_batch = len(x)
         return loss   # total, policy, value
 
     def train(self, states, policies, values, epochs=1, batch=128, seed=0):
@@ -456,6 +472,15 @@ class Learner:
     def grads(self):
         out = np.zeros(self.n, np.float32)
         _check(lib().spai_learner_grads(self.h, _p(out), self.n))
+        return out
+
+    def activation(self, layer):
+        """the last train_batch's post-ReLU activations of conv `layer` (stem, residual
+        convs, policy head, value head), [B][co][6][7]"""
+        nl = 2 * self.blocks + 3
+        co = 32 if layer == nl - 2 else 3 if layer == nl - 1 else self.hidden
+        out = np.zeros((self.last_batch, co, 6, 7), np.float32)
+        _check(lib().spai_learner_activation(self.h, layer, _p(out), out.size))
         return out
 
     def set_comm(self, rank, world, uid=None):
@@ -550,8 +575,10 @@ def policy_sample(p, temperature, u01):
     return out.value
 
 
-def pipeline_run(init_params, selfplay_devices=(0,), learner_device=0, checkpoint_dir=None, **kw):
-    """train_concurrent (main.rs:137-235) on the device; kw: PipelineConfig fields"""
+def pipeline_run(init_params, selfplay_devices=(0,), learner_device=0, checkpoint_dir=None, events=None, **kw):
+    """train_concurrent (main.rs:137-235) on the device; kw: PipelineConfig fields.
+    events: a list that receives every ring event in ring order as a dict (kind,
+    worker, batch, version, n, positions, ring_size, and copies of the samples)"""
     cfg = PipelineConfig()
     _check(lib().spai_pipeline_config_default(C.byref(cfg)))
     devs = (C.c_int * len(selfplay_devices))(*selfplay_devices)
@@ -561,6 +588,18 @@ def pipeline_run(init_params, selfplay_devices=(0,), learner_device=0, checkpoin
     cfg.checkpoint_dir = os.fsencode(checkpoint_dir) if checkpoint_dir else None
     for k, v in kw.items():
         setattr(cfg, k, v)
+    cb = None
+    if events is not None:
+        def on_event(_user, evp):
+            ev = evp.contents
+            n = int(ev.n)
+            d = {k: int(getattr(ev, k)) for k in ("kind", "worker", "batch", "version", "n", "positions", "ring_size")}
+            d["states"] = np.ctypeslib.as_array(ev.states, (n, 126)).copy() if n else np.zeros((0, 126), np.float32)
+            d["policies"] = np.ctypeslib.as_array(ev.policies, (n, 7)).copy() if n else np.zeros((0, 7), np.float32)
+            d["values"] = np.ctypeslib.as_array(ev.values, (n,)).copy() if n else np.zeros(0, np.float32)
+            events.append(d)
+        cb = OBSERVER(on_event)
+        cfg.observer = C.cast(cb, C.c_void_p)
     p = np.ascontiguousarray(init_params, np.float32)
     st = PipelineStats()
     _check(lib().spai_pipeline_run(C.byref(cfg), _p(p), len(p), C.byref(st)))

@@ -54,6 +54,7 @@ def lib():
         L.spai_chess_net_forward.argtypes = [vp, u32, vp, vp, vp]
         L.spai_chess_predict.argtypes = [vp, u32, u32, vp, vp]
         L.spai_chess_rules_bench.argtypes = [vp, u32, u32, u32, vp]
+        L.spai_chess_perft.argtypes = [vp, u32, C.c_int, vp]
         L.spai_chess_tree_reset.argtypes = [vp, u32, u32]
         L.spai_chess_set_net.argtypes = [vp, vp]
         L.spai_chess_trees_create.argtypes = [vp, u32]
@@ -183,6 +184,12 @@ class ChessEngine:
         ms = np.zeros(2, np.float64)
         _check(lib().spai_chess_rules_bench(self.h, first, n, iters, _p(ms)))
         return ms
+
+    def perft(self, depth, slot=0):
+        """[perft(1), ..., perft(depth)] of slot `slot`'s position, on the device"""
+        out = np.zeros(depth, np.uint64)
+        _check(lib().spai_chess_perft(self.h, slot, depth, _p(out)))
+        return [int(v) for v in out]
 
     def encode(self, n, first=0):
         out = np.zeros((n, 19, 8, 8), np.float32)

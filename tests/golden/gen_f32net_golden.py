@@ -10,8 +10,12 @@ SelfPlayWorker::self_play (learner_concurrent.rs:169-242) with Model::predict
 (model/mod.rs:36-98) as the evaluator.  The oracle takes ~12 ms per 2-block
 forward, too slow to run at these sizes inside the GPU suite, hence a fixture.
 
+Two fixtures: mcts_f32net.npz (2 blocks, 48 roots x 64 sims, 6 games x 16 sims)
+and mcts_f32net_6x64.npz (the benchmarked 6x64 net, 24 roots x 128 sims, 4 games
+x 32 sims):  python gen_f32net_golden.py [--six]
+
 Contents:
-  blocks, seed           2-block x 64 net from the shared init stream (spai_net_init_params)
+  blocks, seed           blocks x 64 net from the shared init stream (spai_net_init_params)
   roots [R][3]           (x, o, n) ongoing positions after 0..13 random plies
   sims                   simulations per search
   visits [R][7], policy [R][7], n_children [R]
@@ -27,8 +31,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
 import oracle  # noqa: E402
 
-BLOCKS, SEED, R, SIMS = 2, 7, 48, 64
-SP_GAMES, SP_SIMS, SP_SEED = 6, 16, 21
+SETS = {
+    "mcts_f32net.npz": dict(blocks=2, seed=7, roots=48, sims=64, sp_games=6, sp_sims=16, sp_seed=21),
+    "mcts_f32net_6x64.npz": dict(blocks=6, seed=0, roots=24, sims=128, sp_games=4, sp_sims=32, sp_seed=5),
+}
 
 
 def roots(n, seed):
@@ -46,20 +52,27 @@ def roots(n, seed):
     return out
 
 
-def main():
-    params = oracle.init_params(oracle.GAME_CONNECT4, BLOCKS, 64, SEED)
-    net = oracle.Net(oracle.GAME_CONNECT4, BLOCKS, 64, params)
-    rs = roots(R, 3)
-    rc, pol, ids, vis, nc = oracle.search_c4(rs, SIMS, eval_kind=oracle.EVAL_NET, net=net)
+def make(name, blocks, seed, roots_n, sims, sp_games, sp_sims, sp_seed):
+    params = oracle.init_params(oracle.GAME_CONNECT4, blocks, 64, seed)
+    net = oracle.Net(oracle.GAME_CONNECT4, blocks, 64, params)
+    rs = roots(roots_n, 3)
+    rc, pol, ids, vis, nc = oracle.search_c4(rs, sims, eval_kind=oracle.EVAL_NET, net=net)
     assert rc >= 0, rc   # number of leaves evaluated
-    sp = oracle.self_play(oracle.GAME_CONNECT4, SP_GAMES, SP_SIMS, SP_SEED, eval_kind=oracle.EVAL_NET, net=net,
+    sp = oracle.self_play(oracle.GAME_CONNECT4, sp_games, sp_sims, sp_seed, eval_kind=oracle.EVAL_NET, net=net,
                           max_plies=42)
     np.savez_compressed(
-        os.path.join(HERE, "mcts_f32net.npz"), blocks=BLOCKS, seed=SEED,
-        roots=np.array([[*s.bitboards(), s.n] for s in rs], np.uint64), sims=SIMS, visits=vis, policy=pol,
-        n_children=nc, sp_games=SP_GAMES, sp_sims=SP_SIMS, sp_seed=SP_SEED, sp_enc=sp["enc"], sp_policy=sp["policy"],
+        os.path.join(HERE, name), blocks=blocks, seed=seed,
+        roots=np.array([[*s.bitboards(), s.n] for s in rs], np.uint64), sims=sims, visits=vis, policy=pol,
+        n_children=nc, sp_games=sp_games, sp_sims=sp_sims, sp_seed=sp_seed, sp_enc=sp["enc"], sp_policy=sp["policy"],
         sp_value=sp["value"], sp_game=sp["game"], sp_moves=sp["moves"], sp_n_moves=sp["n_moves"])
-    print("wrote mcts_f32net.npz:", R, "roots,", len(sp["value"]), "self-play samples")
+    print("wrote", name, ":", roots_n, "roots,", len(sp["value"]), "self-play samples")
+
+
+def main():
+    names = ["mcts_f32net_6x64.npz"] if "--six" in sys.argv else list(SETS)
+    for name in names:
+        c = SETS[name]
+        make(name, c["blocks"], c["seed"], c["roots"], c["sims"], c["sp_games"], c["sp_sims"], c["sp_seed"])
 
 
 if __name__ == "__main__":

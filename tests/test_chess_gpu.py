@@ -374,3 +374,21 @@ def test_chess_tree_reset_from_slot_matches_oracle(ch, sc):
         eng.tree_reset(0, n)          # slot out of range
     ch.arena_reset()
     eng.close()
+
+
+def test_device_perft_public_counts(ch, sc):
+    """the device move generator and make-move (wave_movegen / apply_move, the code
+    the search runs) against the public perft counts (chessprogramming.org): the
+    start position to depth 6 (119,060,324), Kiwipete to 5 (193,690,690) and
+    positions 3-6 to depth 5-6 -- breadth-first on the device, every ply's
+    positions in HBM (spai_chess_perft)"""
+    from test_chess_oracle import PERFT
+    eng = sc.ChessEngine(num_searches=4, max_trees=4, eval_kind=sc.EVAL_HASH, max_moves=64)
+    eng.games_resize(len(PERFT))
+    eng.games_write(np.array([_abi_state(ch.ChessState(fen=f, made=0, fifty=0).st) for f, _ in PERFT],
+                             sc.STATE_DTYPE))
+    for i, (fen, counts) in enumerate(PERFT):
+        assert eng.perft(len(counts), slot=i) == counts, fen
+    with pytest.raises(sc.SpaiError):
+        eng.perft(9)
+    eng.close()

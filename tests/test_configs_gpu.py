@@ -1,0 +1,110 @@
+"""BASELINE configs 3 and 5 at their per-GPU shape on one MI355X, checked by
+properties (the oracle cannot replay 4096 x 800 searches; the bit-exact checks
+of search, self-play and the train step are in test_gpu_parity.py /
+test_gpu_fp32.py at smaller sizes).
+
+* C3 slice (BASELINE config 3, one rank's share): 4096 games x 800 sims with
+  the 6x64 bf16 net, the (positions as f32 * 0.3) as usize subsample into the
+  replay ring, 20 learner steps of 128 through a 1-rank RCCL communicator, the
+  RCCL broadcast refresh, and a second round on the refreshed net
+  (self-play-ai_amd/selfplay_dp.py, learner_concurrent.rs:72-85,158-159,169-290).
+  The 1-rank DP learner must stay bit-identical to a plain learner fed the same
+  batches, and the refreshed self-play net must equal a net built from the
+  learner's parameters.
+* C5 at SURVEY §8d's per-GPU shape (train_concurrent, main.rs:137-235):
+  4096-game self-play workers at 800 sims, 6x64, batch 128, 20 x 10 train
+  iterations, ring 12,800; every ring event replayed through the HeapRb model
+  (tests/pipeline_model.py).
+* C5 with several self-play workers on one device (main.rs:169-186 runs 6):
+  three workers' pushes interleave in the ring, checked the same way.
+"""
+import numpy as np
+import pytest
+
+from pipeline_model import check_events, subsample_size
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def spai():
+    import spai as s
+    s.lib()
+    return s
+
+
+def test_c3_slice_full_size(spai, oracle):
+    from selfplay_dp import Config3Rank
+    G, sims, B, K = 4096, 800, 128, 20
+    R = Config3Rank(0, 1, spai.comm_unique_id(), games=G, sims=sims, blocks=6, batch=B, train_steps=K, seed=0)
+    plain = spai.Learner(R.eng, 6, spai.init_params(6, 64, seed=0))   # no communicator
+    ring_twin = spai.Replay(B * 100)
+    for rnd in range(2):
+        games, st, loss, k = R.run_round(collect_games=True)
+        assert st["games"] == G and len(games) == G
+        positions = sum(len(g["moves"]) for g in games)
+        assert st["positions"] == positions and st["sims"] == sims * positions
+        assert k == subsample_size(positions, 0.3)
+        assert np.all(np.isfinite(loss)) and loss[0] > 0
+        # outcomes replay legally in the oracle (every 64th game; all of them in test_fullsize_gpu)
+        for g in games[::64]:
+            s = oracle.C4()
+            for a in g["moves"]:
+                assert a in s.valid_actions()
+                s = s.next_state(int(a))
+            assert s.status != 0
+        # the plain learner, fed the same FIFO batches, stays bit-identical to the
+        # 1-rank RCCL learner (all-reduce weight B/sum(B) = 1, broadcast a no-op)
+        enc = np.concatenate([g["enc"] for g in games])
+        pol = np.concatenate([g["policy"] for g in games])
+        val = np.concatenate([g["value"] for g in games])
+        keep = spai.choose_multiple(len(val), k, seed=0, stream=rnd).astype(np.int64)
+        ring_twin.push(enc[keep], pol[keep], val[keep])
+        for _ in range(K):
+            plain.train_batch(*ring_twin.pop(B))
+        np.testing.assert_array_equal(plain.params(), R.params)
+        # the refreshed self-play net is the learner's weights
+        x = enc[:64].reshape(-1, 3, 6, 7)
+        fresh = spai.Net(R.eng, 6, R.learner.params())
+        lg_a, v_a = R.net.forward(x)
+        lg_b, v_b = fresh.forward(x)
+        fresh.close()
+        np.testing.assert_array_equal(lg_a, lg_b)
+        np.testing.assert_array_equal(v_a, v_b)
+    assert R.totals["samples_trained"] == 2 * K * B
+    assert not np.array_equal(R.params, spai.init_params(6, 64, seed=0))
+    ring_twin.close()
+    plain.close()
+    R.close()
+
+
+def test_c5_pipeline_full_shape(spai):
+    """one 4096-game worker (4096 games per self-play GPU), 800 sims,
+    6x64, batch 128, 20 batches x 10 iterations, ring 12,800"""
+    p0 = spai.init_params(6, 64, seed=3)
+    events = []
+    st = spai.pipeline_run(p0, selfplay_devices=(0,), learner_device=0, games_per_batch=4096, num_searches=800,
+                           batch_size=128, batches_per_iter=20, train_iters=10, replay_capacity=12800, blocks=6,
+                           seed=4, events=events)
+    r = check_events(events, st, capacity=12800, batch_size=128, fraction=0.3, batches_expected=200, workers=1)
+    assert st["weight_version_published"] == 10
+    assert r["overwritten"] > 0            # a 4096-game batch pushes ~30k samples into 12.8k slots
+    assert st["games"] == 4096 * r["pushes"]
+    assert all(np.isfinite(st["last_loss"])) and st["last_loss"][0] > 0
+
+
+def test_c5_pipeline_several_workers_one_device(spai, tmp_path):
+    """three self-play workers (engines on their own host threads) sharing device 0
+    with the learner; their pushes interleave in the one ring"""
+    p0 = spai.init_params(2, 64, seed=5)
+    events = []
+    st = spai.pipeline_run(p0, selfplay_devices=(0, 0, 0), learner_device=0, checkpoint_dir=str(tmp_path),
+                           games_per_batch=64, num_searches=32, batch_size=64, batches_per_iter=4, train_iters=4,
+                           replay_capacity=640, blocks=2, seed=6, events=events)
+    r = check_events(events, st, capacity=640, batch_size=64, fraction=0.3, batches_expected=16, workers=3)
+    assert st["weight_version_published"] == 4
+    assert r["workers_seen"] == 3
+    assert st["games"] == 64 * r["pushes"]
+    for it in range(4):
+        p = spai.load_params(str(tmp_path / ("%d.safetensors" % it)), 2)
+        assert np.isfinite(p).all()

@@ -97,14 +97,20 @@ def test_f32_predict_vs_oracle(spai, oracle):
     e.close()
 
 
-def _golden():
-    return np.load(os.path.join(GOLDEN, "mcts_f32net.npz"))
+# the 2x64 fixture and the benchmarked 6x64 net (gen_f32net_golden.py)
+FIXTURES = ["mcts_f32net.npz", "mcts_f32net_6x64.npz"]
 
 
-def test_f32_net_search_matches_oracle(spai):
+def _golden(name="mcts_f32net.npz"):
+    return np.load(os.path.join(GOLDEN, name))
+
+
+@pytest.mark.parametrize("fixture", FIXTURES)
+def test_f32_net_search_matches_oracle(spai, fixture):
     """Mcts::search with the fp32 net: root visit counts and policies of 48 trees
-    (two search chains) equal the oracle's"""
-    z = _golden()
+    at 64 sims (2x64 net) / 24 trees at 128 sims (6x64), two search chains, equal
+    the oracle's"""
+    z = _golden(fixture)
     roots, sims = z["roots"], int(z["sims"])
     n = len(roots)
     e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_NET, max_moves=2)
@@ -122,10 +128,11 @@ def test_f32_net_search_matches_oracle(spai):
     e.close()
 
 
-def test_f32_net_self_play_matches_oracle(spai):
+@pytest.mark.parametrize("fixture", FIXTURES)
+def test_f32_net_self_play_matches_oracle(spai, fixture):
     """SelfPlayWorker::self_play with the fp32 net: the whole sample stream
     (encodings, visit policies, signed values, moves, emission order)"""
-    z = _golden()
+    z = _golden(fixture)
     n, sims, seed = int(z["sp_games"]), int(z["sp_sims"]), int(z["sp_seed"])
     e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_NET, seed=seed)
     net = spai.Net(e, int(z["blocks"]), spai.init_params(int(z["blocks"]), 64, seed=int(z["seed"])),
@@ -146,11 +153,12 @@ def test_f32_net_self_play_matches_oracle(spai):
     e.close()
 
 
-def test_f32_and_bf16_nets_agree_on_search(spai):
+@pytest.mark.parametrize("fixture", FIXTURES)
+def test_f32_and_bf16_nets_agree_on_search(spai, fixture):
     """the bf16 throughput path against the fp32 path on the same roots: the root
     visit distributions are close (bf16 moves priors by ~1e-2, so visits may
     shift by a few, never the legal-move set)"""
-    z = _golden()
+    z = _golden(fixture)
     roots, sims = z["roots"], int(z["sims"])
     n = len(roots)
     p = spai.init_params(int(z["blocks"]), 64, seed=int(z["seed"]))

@@ -470,19 +470,30 @@ def test_learner_vs_torch_golden(spai):
     e.close()
 
 
-def _check_grads_kinks(g, ref):
-    """fp32 gradient vs the float64 restatement.  Bulk: 3e-4 * max|g| (fp32 through
-    2*blocks+3 layers).  A pre-ReLU value within fp32 rounding of 0 (BN beta is 0 at
-    init, so y = gamma * xhat crosses 0 inside the batch) takes either side of the
-    kink depending on the summation order, and the float64 answer itself jumps by
-    ~5e-4 * max|g| under a 1-ulp parameter perturbation (scripts/learner_conditioning.py:
-    6 blocks / batch 128 gives 4.9e-4, 4.9e-4, 3e-7 for three perturbations).  Such a
-    flip moves the gradients of one channel's weights (2.5e-3 * max|g| measured at
-    2 blocks / batch 128, profiles/r02/learner/dbg_base_2_128.txt), so at most 1 % of
-    the entries may leave the bulk bound, and none may exceed 5e-3 * max|g|."""
+def _check_grads_same_masks(L, g, p0, batch, blocks):
+    """fp32 device gradient vs the float64 restatement run with the DEVICE's ReLU
+    masks (spai_learner_activation > 0).  BN's beta is 0 at init, so some
+    pre-activations sit within fp32 rounding of 0 and take either side of the kink
+    depending on the summation order; forcing the device's side in the
+    restatement removes those flips, so every entry is held to the bulk bound
+    3e-4 * max|g| (fp32 through 2*blocks+3 layers).  The masks may differ from
+    the restatement's own (pre > 0) only where its pre-activation is within
+    1e-4 of its layer's scale of zero: a flip anywhere else fails."""
+    import learner_ref as LR
+    nl = 2 * blocks + 3
+    masks = [L.activation(l) > 0 for l in range(nl)]
+    diag = {}
+    n = len(p0)
+    _, _, _, _, ref = LR.train_step(p0, np.zeros(n), np.zeros(n), 0, *batch, blocks, 64, masks=masks, diag=diag)
+    flips = 0
+    for l in range(nl):
+        pre = diag["pre"][l]
+        diff = masks[l] != (pre > 0)
+        flips += int(diff.sum())
+        assert np.all(np.abs(pre[diff]) <= 1e-4 * np.abs(pre).max()), (l, np.abs(pre[diff]).max())
     d, m = np.abs(g - ref), np.abs(ref).max()
-    assert d.max() <= 5e-3 * m, d.max() / m
-    assert np.mean(d > 3e-4 * m) <= 0.01, np.mean(d > 3e-4 * m)
+    assert d.max() <= 3e-4 * m, (d.max() / m, flips)
+    return flips
 
 
 @pytest.mark.parametrize("blocks,B,steps", [(2, 48, 2), (6, 128, 1), (2, 128, 1), (0, 5, 1)])
@@ -507,11 +518,11 @@ def test_learner_vs_oracle(spai, oracle, blocks, B, steps):
     L = spai.Learner(e, blocks, p0)
     dev_losses = [L.train_batch(*b) for b in batches[:1]]
     g1 = L.grads()
+    _check_grads_same_masks(L, g1, p0, batches[0], blocks)   # reads the first step's activations
     dev_losses += [L.train_batch(*b) for b in batches[1:]]
     P_ref, ref_losses, ref_grads = LR.train(p0, batches, blocks, 64)
     np.testing.assert_allclose(dev_losses[0], ref_losses[0], rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(np.array(dev_losses), ref_losses, rtol=1e-3, atol=1e-4)
-    _check_grads_kinks(g1, ref_grads[0])
     check_learner_params(L.params(), P_ref, ref_grads, blocks, 64, steps, tol=1e-4)
     L.close()
     e.close()
@@ -569,15 +580,20 @@ def test_pipeline_concurrent(spai, tmp_path):
     """train_concurrent (main.rs:137-235) end to end on one GPU: a self-play worker
     thread feeding the replay ring, the learner training batches from it, weights
     published per iteration and picked up by self-play, checkpoints written"""
+    from pipeline_model import check_events
     blocks = 1
     p0 = spai.init_params(blocks, 64, seed=11)
+    events = []
     st = spai.pipeline_run(p0, selfplay_devices=(0,), learner_device=0, checkpoint_dir=str(tmp_path),
                            games_per_batch=32, num_searches=16, batch_size=32, batches_per_iter=3, train_iters=3,
-                           replay_capacity=320, blocks=blocks, seed=2)
+                           replay_capacity=320, blocks=blocks, seed=2, events=events)
     assert st["batches_trained"] == 9
     assert st["weight_version_published"] == 3
     assert st["games"] >= 32 and st["positions"] > 0
-    assert st["samples_pushed"] == pytest.approx(st["samples_pushed"])
+    # every push / pop against the HeapRb model: subsample sizes, FIFO batches bit for
+    # bit, ring sizes, overwrites, weight versions (tests/pipeline_model.py)
+    r = check_events(events, st, capacity=320, batch_size=32, fraction=0.3, batches_expected=9, workers=1)
+    assert r["pushes"] * 32 == st["games"]
     assert all(np.isfinite(st["last_loss"])) and st["last_loss"][0] > 0
     for it in range(3):
         p = spai.load_params(str(tmp_path / ("%d.safetensors" % it)), blocks)

@@ -249,15 +249,16 @@ def test_learner_oracle_vs_torch_golden(oracle):
     check_learner_params(P3, z["params3"], [g_ref], blocks, hidden, 3, tol=1e-4)
 
 
-def test_mcts_f32net_fixture(oracle):
-    """tests/golden/mcts_f32net.npz (search with the fp32 net, gen_f32net_golden.py)
-    is reproducible by the oracle: the first 6 roots"""
-    z = np.load(os.path.join(GOLDEN, "mcts_f32net.npz"))
+@pytest.mark.parametrize("fixture,k", [("mcts_f32net.npz", 6), ("mcts_f32net_6x64.npz", 1)])
+def test_mcts_f32net_fixture(oracle, fixture, k):
+    """tests/golden/mcts_f32net*.npz (search with the fp32 net, gen_f32net_golden.py)
+    is reproducible by the oracle: the first k roots"""
+    z = np.load(os.path.join(GOLDEN, fixture))
     blocks, seed, sims = int(z["blocks"]), int(z["seed"]), int(z["sims"])
     net = oracle.Net(oracle.GAME_CONNECT4, blocks, 64, oracle.init_params(oracle.GAME_CONNECT4, blocks, 64, seed))
     L = oracle.lib()
     roots = []
-    for x, o, n in z["roots"][:6]:
+    for x, o, n in z["roots"][:k]:
         st = oracle.C4State()
         L.or_c4_init(oracle.C.byref(st))
         for col in range(7):
@@ -272,5 +273,32 @@ def test_mcts_f32net_fixture(oracle):
         roots.append(oracle.C4(st))
     rc, pol, ids, vis, nc = oracle.search_c4(roots, sims, eval_kind=oracle.EVAL_NET, net=net)
     assert rc >= 0
-    np.testing.assert_array_equal(vis, z["visits"][:6])
-    np.testing.assert_array_equal(pol, z["policy"][:6])
+    np.testing.assert_array_equal(vis, z["visits"][:k])
+    np.testing.assert_array_equal(pol, z["policy"][:k])
+
+
+def test_learner_ref_mask_override_is_identity_with_own_masks():
+    """learner_ref.train_step(masks=...) with the restatement's own (pre > 0) masks
+    reproduces the plain step exactly (the GPU gradient test forces the device's
+    masks through this path)"""
+    import learner_ref as LR
+    import oracle as O
+    blocks, B = 1, 6
+    rng = np.random.default_rng(0)
+    p0 = O.init_params(O.GAME_CONNECT4, blocks, 64, 3)
+    x = (rng.random((B, 126)) < 0.3).astype(np.float32)
+    pi = rng.random((B, 7))
+    pi /= pi.sum(1, keepdims=True)
+    z = rng.choice([-1.0, 0.0, 1.0], B)
+    n = len(p0)
+    diag = {}
+    P1, _, _, l1, g1 = LR.train_step(p0, np.zeros(n), np.zeros(n), 0, x, pi, z, blocks, 64, diag=diag)
+    masks = [pre > 0 for pre in diag["pre"]]
+    P2, _, _, l2, g2 = LR.train_step(p0, np.zeros(n), np.zeros(n), 0, x, pi, z, blocks, 64, masks=masks)
+    np.testing.assert_array_equal(g1, g2)
+    np.testing.assert_array_equal(P1, P2)
+    np.testing.assert_array_equal(l1, l2)
+    flipped = [m.copy() for m in masks]
+    flipped[1].flat[0] = ~flipped[1].flat[0]          # one forced flip changes the gradient
+    _, _, _, _, g3 = LR.train_step(p0, np.zeros(n), np.zeros(n), 0, x, pi, z, blocks, 64, masks=flipped)
+    assert not np.array_equal(g1, g3)

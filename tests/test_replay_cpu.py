@@ -56,3 +56,60 @@ def test_choose_multiple():
     for st in range(2000):
         counts[spai.choose_multiple(20, 6, seed=3, stream=st)] += 1
     assert counts.min() > 0.8 * counts.mean() and counts.max() < 1.2 * counts.mean()
+
+
+def _c4_samples(rng, n):
+    s = np.zeros((n, 3, 42), np.float32)
+    cell = rng.integers(0, 3, (n, 42))
+    for c in range(3):
+        s[:, c] = cell == c
+    p = rng.random((n, 7)).astype(np.float32)
+    p /= p.sum(1, keepdims=True)
+    return s.reshape(n, 126), p, rng.choice(np.array([-1, 0, 1], np.float32), n)
+
+
+def test_pipeline_event_model_catches_faults():
+    """tests/pipeline_model.py (the checker of the GPU pipeline tests) accepts a
+    correct HeapRb event stream and rejects a reordered batch, a wrong subsample
+    size and a sample trained before its weights were published"""
+    import copy
+
+    from pipeline_model import POP, PUSH, check_events, subsample_size
+    rng = np.random.default_rng(1)
+    cap, B = 40, 8
+    ring = collections.deque()
+    events, pushed, over, pops = [], 0, 0, 0
+    for b in range(6):
+        pos = int(rng.integers(20, 60))
+        k = subsample_size(pos, 0.3)
+        s, p, v = _c4_samples(rng, k)
+        for i in range(k):
+            if len(ring) == cap:
+                ring.popleft()
+                over += 1
+            ring.append((s[i], p[i], v[i]))
+        pushed += k
+        events.append(dict(kind=PUSH, worker=0, batch=b, version=b // 2, n=k, positions=pos, ring_size=len(ring),
+                           states=s, policies=p, values=v))
+        while len(ring) >= B:
+            got = [ring.popleft() for _ in range(B)]
+            events.append(dict(kind=POP, worker=0, batch=pops, version=b // 2 + 1, n=B, positions=0,
+                               ring_size=len(ring), states=np.stack([g[0] for g in got]),
+                               policies=np.stack([g[1] for g in got]), values=np.array([g[2] for g in got])))
+            pops += 1
+    stats = dict(samples_pushed=pushed, samples_overwritten=over, batches_trained=pops,
+                 positions=sum(e["positions"] for e in events if e["kind"] == PUSH))
+    check_events(events, stats, cap, B, 0.3, batches_expected=pops, workers=1)
+    first_pop = next(i for i, e in enumerate(events) if e["kind"] == POP)
+    bad = copy.deepcopy(events)                       # two samples of a batch swapped
+    bad[first_pop]["states"][[0, 1]] = bad[first_pop]["states"][[1, 0]]
+    with pytest.raises(AssertionError):
+        check_events(bad, stats, cap, B, 0.3)
+    bad = copy.deepcopy(events)                       # (positions * 0.3) as usize violated
+    bad[0]["positions"] += 10
+    with pytest.raises(AssertionError):
+        check_events(bad, stats, cap, B, 0.3)
+    bad = copy.deepcopy(events)                       # played with weights not yet published
+    bad[0]["version"] = 99
+    with pytest.raises(AssertionError):
+        check_events(bad, stats, cap, B, 0.3)
