@@ -54,7 +54,7 @@ impl Default for Args {
 }
 
 /// A root or root child as last seen by the host (the engine holds the rest).
-/// `device_id` is the engine's node id (Connect4) or child index (TicTacToe).
+/// `device_id` is the engine's node id (Connect4) or root-child index (TicTacToe, chess).
 #[derive(Clone, Default)]
 pub struct Node<T: State> {
     pub state: T,
@@ -65,7 +65,7 @@ pub struct Node<T: State> {
 }
 
 /// Where a searched tree lives: an engine handle (spai_engine* for Connect4,
-/// spai_ttt* for TicTacToe) and the tree's slot in it.
+/// spai_ttt* for TicTacToe, spai_chess* for chess) and the tree's slot in it.
 #[derive(Clone, Copy, PartialEq, Eq, Debug)]
 pub struct DeviceBinding {
     pub engine: usize,
@@ -116,6 +116,8 @@ impl<T: State> Tree<T> {
                 match b.game {
                     sys::SPAI_GAME_CONNECT4 => sys::spai_tree_use_subtree(b.engine as *mut sys::spai_engine, b.slot,
                                                                           child.device_id),
+                    sys::SPAI_GAME_CHESS => sys::spai_chess_tree_use_subtree(b.engine as *mut sys::spai_chess, b.slot,
+                                                                             child.device_id),
                     _ => sys::spai_ttt_tree_use_subtree(b.engine as *mut sys::spai_ttt, b.slot, child.device_id),
                 }
             };
@@ -133,20 +135,15 @@ impl<T: State> Tree<T> {
     }
 }
 
-/// The device half of a Net: how its engine searches a batch of trees.  The
-/// Connect4 and TicTacToe nets (model/connect_four.rs, model/tictactoe.rs)
-/// implement it over spai_search / spai_ttt_search.
-pub trait DeviceSearch: Net {
-    fn search_trees(&self, args: &Args, trees: &mut [&mut Tree<Self::State>])
-        -> Vec<(<Self::State as State>::Policy, Vec<(usize, f32)>)>;
-}
-
 pub struct Mcts<T: Net> {
     pub args: Args,
     pub model: Model<T>,
 }
 
-impl<T: Net + DeviceSearch> Mcts<T> {
+// The device search is a provided method of Net (model/mod.rs), overridden by the
+// Connect4, TicTacToe and chess nets, so this impl keeps the reference's bound and
+// learner.rs / learner_concurrent.rs compile unchanged.
+impl<T: Net> Mcts<T> {
     /// Mcts::search (mcts.rs:196-332): `num_searches` iterations over every tree
     /// on the device, then per tree (normalized root visit policy,
     /// [(root-child id, visits)]) in the trees' order.

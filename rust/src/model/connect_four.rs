@@ -4,7 +4,7 @@
 //! model/connect_four.rs:50-72 (so the VarStore, its checkpoints and the
 //! trainer's `forward(x, true)` are unchanged), and keeps shallow handles to
 //! every variable in construction order.  Inference runs on the MI355X:
-//! `forward(x, false)` and the search (mcts::DeviceSearch) go through libspai
+//! `forward(x, false)` and the search (`Net::search_trees`) go through libspai
 //! with a device copy of the weights, rebuilt whenever the VarStore's values
 //! change (the trainer -> self-play weight copy of learner_concurrent.rs:158-159
 //! needs no extra call).  bf16 MFMA by default; SPAI_DTYPE=f32 selects the
@@ -16,7 +16,7 @@ use tch::{Device, Kind, Tensor};
 
 use crate::game::connect_four::{self, State as C4State};
 use crate::game::{Policy as _, State as _};
-use crate::mcts::{Args as MctsArgs, DeviceBinding, DeviceSearch, Node, Tree};
+use crate::mcts::{Args as MctsArgs, DeviceBinding, Node, Tree};
 use crate::mcts::spai_sys as sys;
 
 pub struct Args {
@@ -126,6 +126,11 @@ impl super::Net for Net {
         (Tensor::from_slice(&logits).view((n, 7)).to_device(x.device()),
          Tensor::from_slice(&value).view((n, 1)).to_device(x.device()))
     }
+
+    fn search_trees(&self, args: &MctsArgs, trees: &mut [&mut Tree<C4State>])
+        -> Vec<super::SearchResult<C4State>> {
+        self.device_search(args, trees)
+    }
 }
 
 impl Net {
@@ -185,9 +190,9 @@ impl Net {
     }
 }
 
-impl DeviceSearch for Net {
+impl Net {
     // Mcts::search (mcts.rs:196-332) for Connect4 trees, all on the device
-    fn search_trees(&self, args: &MctsArgs, trees: &mut [&mut Tree<C4State>])
+    fn device_search(&self, args: &MctsArgs, trees: &mut [&mut Tree<C4State>])
         -> Vec<(connect_four::Policy, Vec<(usize, f32)>)> {
         let n = trees.len();
         if n == 0 {

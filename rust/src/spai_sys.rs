@@ -37,6 +37,37 @@ pub struct spai_ttt_state {
     pub pad: [u8; 2],
 }
 
+/// spai_chess_state (include/spai.h): bitboards in chess::Piece / Color order
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug, PartialEq, Eq)]
+pub struct spai_chess_state {
+    pub pieces: [u64; 6],
+    pub colors: [u64; 2],
+    pub side: u8,
+    pub castle: u8,
+    pub ep: u8,
+    pub status: u8,
+    pub fifty: u16,
+    pub made: u16,
+    pub reps: u32,
+    pub pad: u32,
+}
+
+impl spai_chess_state {
+    /// the start position (chess::Game::new(), game/chess.rs:94-101)
+    pub fn start() -> Self {
+        Self {
+            pieces: [0x00FF_0000_0000_FF00, 0x4200_0000_0000_0042, 0x2400_0000_0000_0024, 0x8100_0000_0000_0081,
+                     0x0800_0000_0000_0008, 0x1000_0000_0000_0010],
+            colors: [0xFFFF, 0xFFFF_0000_0000_0000],
+            side: 0,
+            castle: 15,
+            ep: 64,
+            ..Default::default()
+        }
+    }
+}
+
 #[repr(C)]
 #[derive(Clone, Copy, Default, Debug)]
 pub struct spai_config {
@@ -76,6 +107,8 @@ pub enum spai_net {}
 pub enum spai_learner {}
 pub enum spai_ttt {}
 pub enum spai_ttt_net {}
+pub enum spai_chess {}
+pub enum spai_chess_net {}
 
 pub type spai_sample_sink = extern "C" fn(
     user: *mut c_void,
@@ -119,12 +152,35 @@ extern "C" {
     pub fn spai_ttt_net_create(e: *mut spai_ttt, blocks: c_int, params: *const f32, n: usize,
                                out: *mut *mut spai_ttt_net) -> c_int;
     pub fn spai_ttt_net_destroy(net: *mut spai_ttt_net) -> c_int;
+    pub fn spai_ttt_net_forward(net: *mut spai_ttt_net, n: u32, x: *const f32, logits: *mut f32, value: *mut f32)
+        -> c_int;
     pub fn spai_ttt_set_net(e: *mut spai_ttt, net: *mut spai_ttt_net) -> c_int;
     pub fn spai_ttt_trees_create(e: *mut spai_ttt, n: u32) -> c_int;
     pub fn spai_ttt_tree_reset(e: *mut spai_ttt, tree: u32, root: *const spai_ttt_state) -> c_int;
     pub fn spai_ttt_search(e: *mut spai_ttt, n: u32, tree_idx: *const u32, num_searches: u32, policy: *mut f32,
                            child_ids: *mut u32, child_visits: *mut f32, n_children: *mut u32) -> c_int;
     pub fn spai_ttt_tree_use_subtree(e: *mut spai_ttt, tree: u32, child_index: u32) -> c_int;
+
+    // chess (game/chess.rs, model/chess.rs): game slots, net, trees
+    pub fn spai_chess_config_default(cfg: *mut spai_config) -> c_int;
+    pub fn spai_chess_create(cfg: *const spai_config, device: c_int, out: *mut *mut spai_chess) -> c_int;
+    pub fn spai_chess_destroy(e: *mut spai_chess) -> c_int;
+    pub fn spai_chess_games_resize(e: *mut spai_chess, n: u32) -> c_int;
+    pub fn spai_chess_games_write(e: *mut spai_chess, first: u32, n: u32, s: *const spai_chess_state) -> c_int;
+    pub fn spai_chess_games_read(e: *mut spai_chess, first: u32, n: u32, s: *mut spai_chess_state) -> c_int;
+    pub fn spai_chess_apply(e: *mut spai_chess, first: u32, n: u32, moves: *const u16, rc: *mut i32) -> c_int;
+    pub fn spai_chess_net_create(e: *mut spai_chess, blocks: c_int, params: *const f32, n: usize,
+                                 out: *mut *mut spai_chess_net) -> c_int;
+    pub fn spai_chess_net_destroy(net: *mut spai_chess_net) -> c_int;
+    pub fn spai_chess_net_forward(net: *mut spai_chess_net, n: u32, x: *const f32, logits: *mut f32, value: *mut f32)
+        -> c_int;
+    pub fn spai_chess_set_net(e: *mut spai_chess, net: *mut spai_chess_net) -> c_int;
+    pub fn spai_chess_trees_create(e: *mut spai_chess, n: u32) -> c_int;
+    pub fn spai_chess_tree_reset(e: *mut spai_chess, tree: u32, slot: u32) -> c_int;
+    pub fn spai_chess_search(e: *mut spai_chess, n: u32, tree_idx: *const u32, num_searches: u32, policy: *mut f32,
+                             child_ids: *mut u32, child_visits: *mut f32, child_moves: *mut u16,
+                             n_children: *mut u32) -> c_int;
+    pub fn spai_chess_tree_use_subtree(e: *mut spai_chess, tree: u32, child_index: u32) -> c_int;
 
     // Policy trait helpers on a flat policy (game/mod.rs:35-44)
     pub fn spai_policy_normalize(p: *mut f32, n: u32) -> c_int;
