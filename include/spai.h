@@ -209,8 +209,12 @@ int spai_engine_timing_items(spai_engine *eng, double *total_ms, double *items);
  * stamps at every phase boundary of the fused kernel.  cycles[k] (k < 20) = mean
  * shader cycles from group start to stamp k (0 start, 1 stem, 2..13 residual
  * convs, 14 head conv, 15 linears, 16 end; 17/18/19 = block 0 conv1 k-loop end,
- * epilogue end, barrier passed).  Needs the diagnostic build (SPAI_DIAG);
- * the production library returns SPAI_ERR_UNSUPPORTED.  Never on the timed path. */
+ * epilogue end, barrier passed).  Wall clock (s_memrealtime): cycles[20] = shader
+ * cycles from kernel entry to the first group's start, [21] the same in ns, [22] ns
+ * from the first group's start to the workgroup's end, [23] ns from the earliest
+ * entry to the latest end over the launch.  cycles holds 24 doubles.  Needs the
+ * diagnostic build (SPAI_DIAG); the production library returns
+ * SPAI_ERR_UNSUPPORTED.  Never on the timed path. */
 int spai_net_phase_cycles(spai_net *net, uint32_t count, double *cycles);
 /* Device time of the search's forward launch ALONE (nothing else on the GPU):
  * ms = mean over `iters` back-to-back launches on `count` random reachable

@@ -10,6 +10,11 @@ if [ -n "${TESTS:-}" ]; then
       > $O/pytest.log 2>&1
   rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
 fi
+if [ -n "${PHASES:-}" ]; then   # per-phase stamps of the diagnostic build (make -C self-play-ai_amd diag)
+  SPAI_LIB=$PWD/build_exp/libspai_diag.so timeout -k 10 180 python scripts/net_phases.py > $O/phases.txt 2>&1 \
+      || { cat $O/phases.txt; exit 1; }
+  cat $O/phases.txt
+fi
 libs=$(for v in $VARS; do printf "build_exp/libspai_%s.so," $v; done)
 timeout -k 10 300 python scripts/fwd_sweep.py --libs ${libs%,} --counts ${COUNTS:-256,512,1006,1500,2048,4096} \
     > $O/sweep.txt 2>&1 || { tail -5 $O/sweep.txt; exit 1; }

@@ -22,7 +22,9 @@ for S in range(1, 9):
     d = np.diff(c[:17])
     print(f"S={S}: {c[16]:.0f} cycles/wave = {c[16] / 2.1e3:.1f} us @2.1GHz  stem {d[0]:.0f} res0 {d[1]:.0f} "
           f"res1 {d[2]:.0f} res2 {d[3]:.0f} head {d[13]:.0f} linear {d[14]:.0f} end {d[15]:.0f}; "
-          f"block0 conv1: k-loop {c[17] - c[1]:.0f}, epilogue {c[18] - c[17]:.0f}, barrier {c[19] - c[18]:.0f}")
+          f"block0 conv1: k-loop {c[17] - c[1]:.0f}, epilogue {c[18] - c[17]:.0f}, barrier {c[19] - c[18]:.0f}; "
+          f"wall: entry->group {c[21] / 1e3:.2f} us ({c[20]:.0f} cyc), group {c[22] / 1e3:.2f} us, "
+          f"launch span {c[23] / 1e3:.2f} us, clock {c[16] / max(c[22], 1):.2f} GHz")
 os.environ.pop("SPAI_PHASE_S")
 net.close()
 e.close()

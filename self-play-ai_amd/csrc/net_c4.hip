@@ -76,7 +76,9 @@ constexpr int kBias = kL + kWaves * 64 * 4; // all conv biases, staged once per 
 constexpr int kPlanes = kBias + kBiasFloats * 4;   // stem neighbour planes [8][32] u64
 constexpr int kWStem = kPlanes + kS * 32 * 8;      // stem weight fragments [4 ct][64 lanes] x 16 B, staged once
 constexpr int kLdsBytes = kWStem + 4 * 64 * 16;
-constexpr int kStamps = 20;                // phase stamps per wave in the diagnostic mode (17..19: inside block 0 conv1)
+constexpr int kStamps = 24;                // phase stamps per wave in the diagnostic mode (17..19: inside block 0 conv1;
+                                           // 20/21: s_memtime / s_memrealtime at kernel entry, 22: s_memrealtime at the
+                                           // first group's stamp 0, 23: s_memrealtime after the last group)
 static_assert(kS * kLinPitch * 2 <= kHBytes, "head features fit in Y");
 static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 
@@ -105,6 +107,13 @@ constexpr bool kDiagHead = false;
 __device__ __forceinline__ void stamp(const NetParams &P, int wave, int lane, int k) {
 #ifdef SPAI_DIAG
     if (P.stamps && lane == 0) P.stamps[((size_t)blockIdx.x * kWaves + wave) * kStamps + k] = __builtin_amdgcn_s_memtime();
+#endif
+}
+// wall-clock stamp (100 MHz constant clock), diagnostic build only
+__device__ __forceinline__ void stamp_real(const NetParams &P, int wave, int lane, int k) {
+#ifdef SPAI_DIAG
+    if (P.stamps && lane == 0)
+        P.stamps[((size_t)blockIdx.x * kWaves + wave) * kStamps + k] = __builtin_amdgcn_s_memrealtime();
 #endif
 }
 
@@ -626,6 +635,8 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
                                                       NetParams P, float *__restrict__ priors,
                                                       float *__restrict__ value, float *__restrict__ logits) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
+    stamp(P, threadIdx.x >> 6, threadIdx.x & 63, 20);
+    stamp_real(P, threadIdx.x >> 6, threadIdx.x & 63, 21);
     const uint32_t count = count_ptr ? *count_ptr : count_imm;
     const int S = force_s > 0 ? force_s : group_size(count, gridDim.x);
     const int ngroups = (int)((count + S - 1) / S);
@@ -671,6 +682,7 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
         }
         __syncthreads();
         stamp(P, wave, lane, 0);
+        if (grp == (int)blockIdx.x) stamp_real(P, wave, lane, 22);
         // hide the lane id from loop-invariant code motion: hoisting the per-lane
         // geometry out of the group loop would keep it live across every layer
         int ln = lane;
@@ -737,6 +749,7 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
         stamp(P, wave, lane, 16);
         __syncthreads();   // kB / planes / L are rewritten by the next group
     }
+    stamp_real(P, wave, lane, 23);
 }
 
 // ---------------------------------------------------------------- host packing
@@ -1038,17 +1051,27 @@ int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
     std::vector<unsigned long long> hs(d.n);
     SPAI_HIP(hipMemcpyAsync(hs.data(), d.p, d.n * 8, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipStreamSynchronize(st));
-    // cycles[k] = mean over workgroups/waves of stamp[k] - stamp[0]; cycles[kStamps] = mean total
+    // cycles[k], k < 20: mean over workgroups/waves of stamp[k] - stamp[0] (shader clock).
+    // Wall clock (s_memrealtime, 100 MHz): cycles[20] = mean entry -> first group start in
+    // shader cycles, [21] the same in ns, [22] mean first group start -> end in ns, [23] the
+    // launch span (latest end - earliest entry over all workgroups) in ns.
     for (int k = 0; k < kStamps; ++k) cycles[k] = 0;
     double cntw = 0;
+    unsigned long long first_in = ~0ull, last_out = 0;
     for (uint32_t g = 0; g < grid; ++g)
         for (int w = 0; w < kWaves; ++w) {
             const unsigned long long *sp = hs.data() + ((size_t)g * kWaves + w) * kStamps;
             if (!sp[0] || !sp[16]) continue;   // (a workgroup with no group)
-            for (int k = 0; k < kStamps; ++k) cycles[k] += sp[k] ? (double)(sp[k] - sp[0]) : 0.0;
+            for (int k = 0; k < 20; ++k) cycles[k] += sp[k] ? (double)(sp[k] - sp[0]) : 0.0;
+            cycles[20] += (double)(sp[0] - sp[20]);   // (the last group's stamp 0: one group per workgroup in the sweeps)
+            cycles[21] += 10.0 * (double)(sp[22] - sp[21]);
+            cycles[22] += 10.0 * (double)(sp[23] - sp[22]);
+            first_in = std::min(first_in, sp[21]);
+            last_out = std::max(last_out, sp[23]);
             cntw += 1;
         }
-    for (int k = 0; k < kStamps; ++k) cycles[k] /= cntw > 0 ? cntw : 1;
+    for (int k = 0; k < 23; ++k) cycles[k] /= cntw > 0 ? cntw : 1;
+    cycles[23] = last_out > first_in ? 10.0 * (double)(last_out - first_in) : 0.0;
     return SPAI_OK;
 }
 

@@ -257,7 +257,7 @@ class Net:
         return lg, v
 
     def phase_cycles(self, count=4096):
-        c = np.zeros(20, np.float64)
+        c = np.zeros(24, np.float64)
         _check(lib().spai_net_phase_cycles(self.h, count, _p(c)))
         return c
 
