@@ -1,0 +1,135 @@
+"""Cell orders for the fused Connect4 forward (net_c4.hip): which board cell each
+LDS row group holds, per group size S, so that as many 16-row position tiles as
+possible have NO on-board neighbour for some 3x3 tap -- those (tile, tap) MFMAs
+and their B-fragment reads are skipped (the products would be exact zeros).
+
+For S >= 4 (cell-major groups) LDS row r of a group of S positions holds cell
+kCellOrder[S][r / S] of position r % S.  The search maximises the skipped (tile,
+tap) pairs while keeping the four waves' MFMA counts balanced under the kernel's
+task plans (Plan<W, CT, NPT>: co-major for NPT <= 8, pair split up to 11 tiles,
+position-major above), for the trunk convs (CT = 4) and, at a quarter of the
+weight, the head conv (CT = 3).  At S = 4 the order index's parity must equal
+the cell's checkerboard colour (h + w) & 1: a tile then holds row groups 4t..4t+3
+whose neighbours for any tap alternate in parity, which keeps the B-fragment reads
+bank-conflict free (net_c4.hip make_geo).  S <= 3 keep the position-major rows of
+the identity order (16 consecutive cells per tile: no tile lies on one board
+edge, nothing to skip).  Deterministic (fixed seeds); prints the C++ tables.
+    python scripts/gen_cell_orders.py > /tmp/orders.txt
+"""
+import random
+
+R, C = 6, 7
+CELLS = [(h, w) for h in range(R) for w in range(C)]
+TAPS = [(dh, dw) for dh in (-1, 0, 1) for dw in (-1, 0, 1)]   # tap index = (dh+1)*3 + (dw+1), as net_c4.hip
+
+
+def off_board(c, t):
+    return not (0 <= c[0] + t[0] < R and 0 <= c[1] + t[1] < C)
+
+
+def npt(S):
+    return (S * 42 + 15) // 16
+
+
+def plan(W, CT, n):
+    """(position tile, co tile) tasks of wave W: net_c4.hip Plan<W, CT, NPT>"""
+    mode = 1 if n <= 8 else (2 if CT == 4 and n <= 11 else 0)
+    tt = n * CT
+    if mode == 2:
+        m, r, pj, ph = n // 2, n % 2, W >> 1, W & 1
+        return [(ph * m + i // 2, 2 * pj + (i & 1)) if i < 2 * m else (n - 1, 2 * pj + ph) for i in range(2 * m + r)]
+    first, nr = tt * W // 4, tt * (W + 1) // 4 - tt * W // 4
+    if mode == 1:
+        return [((first + i) % n, (first + i) // n) for i in range(nr)]
+    return [((first + i) // CT, (first + i) % CT) for i in range(nr)]
+
+
+def skip_masks(order, S):
+    out = []
+    for t in range(npt(S)):
+        m = 0
+        for ti, tap in enumerate(TAPS):
+            rows = [r for r in range(16 * t, 16 * t + 16) if r < 42 * S]
+            if rows and all(off_board(order[r // S], tap) for r in rows):
+                m |= 1 << ti
+        out.append(m)
+    return out
+
+
+def cost(order, S, CT=4):
+    masks, n = skip_masks(order, S), npt(S)
+    per = [sum(sum(1 for ti in range(9) if not (masks[pt] >> ti) & 1) for pt, _ in plan(W, CT, n)) for W in range(4)]
+    return max(per), per, masks
+
+
+def score(order, S):
+    return cost(order, S)[0] + 0.25 * cost(order, S, 3)[0]
+
+
+def colour_ok(o):
+    return all(((h + w) & 1) == (i & 1) for i, (h, w) in enumerate(o))
+
+
+def search(S, iters, seed):
+    rnd = random.Random(seed)
+    checker = S == 4
+    ring = ([(0, w) for w in range(7)] + [(h, 6) for h in range(1, 6)] + [(5, w) for w in range(5, -1, -1)]
+            + [(h, 0) for h in range(4, 0, -1)])
+    inner = [(h, w) for h in range(1, 5) for w in range(1, 6)]
+    best = None
+    for start in range(22):
+        for d in (1, -1):
+            rr = [ring[(start + d * i) % 22] for i in range(22)]
+            for split in range(23):
+                o = rr[:split] + inner[:10] + rr[split:] + inner[10:]
+                if checker:   # re-deal the cells onto the indices of their colour, keeping their relative order
+                    black = [x for x in o if not (x[0] + x[1]) & 1]
+                    white = [x for x in o if (x[0] + x[1]) & 1]
+                    o = [black[i // 2] if i % 2 == 0 else white[i // 2] for i in range(42)]
+                c = score(o, S)
+                if best is None or c < best[0]:
+                    best = (c, o)
+    cur, curc = list(best[1]), best[0]
+    for _ in range(iters):
+        i, j = rnd.randrange(42), rnd.randrange(42)
+        if checker and (i & 1) != (j & 1):
+            continue
+        cur[i], cur[j] = cur[j], cur[i]
+        c = score(cur, S)
+        if c <= curc:
+            curc = c
+        else:
+            cur[i], cur[j] = cur[j], cur[i]
+    return curc, cur
+
+
+def main():
+    orders, masks = {}, {}
+    for S in range(1, 9):
+        if S <= 3:   # position-major rows: nothing to skip
+            o = list(CELLS)
+            orders[S], masks[S] = [h * 7 + w for h, w in o], [0] * npt(S)
+            print(f"// S={S}: position-major rows, identity order")
+            continue
+        o = min((search(S, 8000, seed) for seed in range(4)), key=lambda x: x[0])[1]
+        assert S != 4 or colour_ok(o)
+        orders[S] = [h * 7 + w for h, w in o]
+        masks[S] = skip_masks(o, S)
+        new = cost(o, S)
+        print(f"// S={S}: max MFMA tile-taps per wave and trunk layer {cost(CELLS, S)[0]} -> {new[0]} {new[1]}, "
+              f"head {cost(CELLS, S, 3)[0]} -> {cost(o, S, 3)[0]}")
+    print("constexpr uint8_t kCellOrderInit[9][42] = {")
+    print("    {" + ", ".join(["0"] * 42) + "},")
+    for S in range(1, 9):
+        print("    {" + ", ".join(map(str, orders[S])) + "},")
+    print("};")
+    print("__host__ __device__ constexpr uint16_t tap_skip(int S, int t) {")
+    for S in range(1, 9):
+        print(f"    constexpr uint16_t m{S}[21] = {{" + ", ".join(map(str, masks[S] + [0] * (21 - len(masks[S])))) + "};")
+    print("    return S == 1 ? m1[t] : S == 2 ? m2[t] : S == 3 ? m3[t] : S == 4 ? m4[t] : S == 5 ? m5[t] : S == 6 ? m6[t]"
+          " : S == 7 ? m7[t] : m8[t];")
+    print("}")
+
+
+if __name__ == "__main__":
+    main()

@@ -65,7 +65,7 @@ constexpr int kHC = 36;                    // channels per cell in H
 constexpr int kLinFeat = kHC * 42;         // 1512
 constexpr int kLinK = 1536;                // padded to 48 k-steps of 32
 constexpr int kLinKSteps = kLinK / 32;     // 48
-constexpr int kLinPitch = kLinK + 8;       // 3088-B rows: 16 rows hit 16 distinct 16-B bank groups
+constexpr int kLinPitch = kLinK + 16;      // the largest head-feature pitch (lin_pitch) sizes the overlay
 constexpr int kH = kY;                     // bf16 head features [8][kLinPitch] overlay Y
 constexpr int kHBytes = kP * 128;          // (all of Y)
 constexpr int kB = kH + kHBytes;           // 8 x (mine, theirs)
@@ -73,9 +73,12 @@ constexpr int kL = kB + kS * 16;           // linear partials [4 waves][8][8] f3
 constexpr int kMaxBlocks = 20;
 constexpr int kBiasFloats = kHid + 2 * kMaxBlocks * kHid + 48;   // stem, residual convs, head
 constexpr int kBias = kL + kWaves * 64 * 4; // all conv biases, staged once per workgroup
-constexpr int kPlanes = kBias + kBiasFloats * 4;   // stem neighbour planes [8][32] u64
-constexpr int kWStem = kPlanes + kS * 32 * 8;      // stem weight fragments [4 ct][64 lanes] x 16 B, staged once
-constexpr int kLdsBytes = kWStem + 4 * 64 * 16;
+constexpr int kPlanes = kBias + kBiasFloats * 4;   // stem neighbour planes [8][34] u64 (272-B rows: positions
+                                                   // in different 16-B bank groups)
+constexpr int kPlaneRow = 34;
+constexpr int kWStem = kPlanes + kS * kPlaneRow * 8;   // stem weight fragments [4 ct][64 lanes] x 16 B, staged once
+constexpr int kTab = kWStem + 4 * 64 * 16;         // the launch's geometry table: [42 row groups] x 16 B (NetParams::geo)
+constexpr int kLdsBytes = kTab + 42 * 16;
 constexpr int kStamps = 24;                // phase stamps per wave in the diagnostic mode (17..19: inside block 0 conv1;
                                            // 20/21: s_memtime / s_memrealtime at kernel entry, 22: s_memrealtime at the
                                            // first group's stamp 0, 23: s_memrealtime after the last group)
@@ -89,9 +92,12 @@ struct NetParams {
     const float *b_stem;   // [64]
     const float *b_res;    // [2*blocks][64]
     const float *b_head;   // [48]
-    const uint4 *w_lin;    // [46 ks][64] B fragments of the fused policy|value linear
+    const uint4 *w_lin;    // [48 ks][64] B fragments of the fused policy|value linear
     const float *b_pol;    // [7]
     const float *b_val;    // [1]
+    // per group size S and row group idx (= LDS row / S): {cell, then the row group
+    // holding each 3x3 tap's neighbour cell as 9 bytes (0xFF off the board)} x 16 B
+    const uint4 *geo;             // [9][42]
     unsigned long long *stamps;   // diagnostic: [grid][4 waves][kStamps] s_memtime, or null
     int blocks;
 };
@@ -129,6 +135,61 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
 __device__ __forceinline__ uint32_t pack_relu_bf16x2(float a, float b) {
     const i16x2 h = __builtin_bit_cast(i16x2, __builtin_convertvector((f32x2){a, b}, bf16x2));
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(h, (i16x2){0, 0}));
+}
+
+// ---------------------------------------------------------------- cell order and skipped taps
+// Row layout of a group of S positions in the activation buffers:
+//  * S <= 3, position-major: row r holds cell r % 42 of position r / 42 (cell =
+//    board row * 7 + column), so a 3x3 tap is a contiguous shift of the rows;
+//  * S >= 4, cell-major: row r holds cell kCellOrder[S][r / S] of position r % S.
+//    The orders group board-edge cells so that some 16-row position tiles have NO
+//    on-board neighbour for a tap: tap_skip(S, t) is the mask of such taps (bit
+//    (dh+1)*3 + (dw+1)) of tile t, and their MFMAs and B-fragment reads are skipped
+//    -- every product they would add is an exact zero (an out-of-board tap reads
+//    the zeroed block), so the results are the same.
+// Generated by scripts/gen_cell_orders.py (balanced over the four waves' task
+// plans; at S = 4 the order index's parity is the cell's checkerboard colour,
+// which keeps the permuted B reads conflict-free); max MFMA (tile, tap) pairs per
+// wave and layer:
+// S=1: position-major rows, identity order
+// S=2: position-major rows, identity order
+// S=3: position-major rows, identity order
+// S=4: max MFMA tile-taps per wave and trunk layer 90 -> 84 [84, 84, 84, 84], head 72 -> 72
+// S=5: max MFMA tile-taps per wave and trunk layer 126 -> 114 [114, 102, 114, 106], head 99 -> 84
+// S=6: max MFMA tile-taps per wave and trunk layer 144 -> 132 [128, 132, 132, 132], head 108 -> 99
+// S=7: max MFMA tile-taps per wave and trunk layer 171 -> 146 [146, 144, 144, 142], head 126 -> 111
+// S=8: max MFMA tile-taps per wave and trunk layer 189 -> 159 [153, 159, 159, 153], head 144 -> 123
+constexpr uint8_t kCellOrder[9][42] = {   // host: packed into NetParams::geo at net_create
+    {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41},
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41},
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 40, 41},
+    {22, 33, 10, 23, 24, 11, 26, 17, 8, 25, 18, 5, 6, 3, 4, 1, 34, 13, 20, 27, 30, 9, 16, 7, 38, 37, 40, 41, 0, 21, 14, 35, 32, 31, 12, 29, 28, 19, 2, 15, 36, 39},
+    {13, 5, 30, 10, 23, 12, 38, 40, 37, 36, 0, 32, 27, 41, 20, 34, 2, 4, 3, 1, 16, 18, 26, 33, 39, 31, 22, 11, 28, 21, 14, 7, 8, 9, 15, 19, 24, 17, 35, 25, 29, 6},
+    {37, 20, 40, 33, 22, 13, 25, 24, 35, 39, 38, 7, 10, 32, 19, 17, 27, 34, 41, 8, 16, 11, 36, 12, 2, 0, 4, 6, 26, 28, 1, 29, 30, 3, 15, 9, 31, 5, 23, 18, 21, 14},
+    {8, 22, 4, 3, 1, 13, 20, 9, 33, 7, 21, 14, 25, 18, 19, 24, 35, 28, 0, 2, 5, 31, 32, 12, 16, 38, 36, 40, 39, 37, 26, 17, 27, 6, 34, 11, 30, 15, 23, 29, 10, 41},
+    {28, 21, 41, 37, 18, 26, 1, 2, 16, 29, 22, 31, 15, 17, 5, 6, 24, 8, 13, 20, 4, 3, 33, 30, 27, 34, 0, 35, 12, 25, 23, 10, 36, 39, 19, 11, 32, 9, 38, 40, 7, 14},
+};
+__host__ __device__ constexpr uint16_t tap_skip(int S, int t) {
+    constexpr uint16_t m1[21] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    constexpr uint16_t m2[21] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    constexpr uint16_t m3[21] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    constexpr uint16_t m4[21] = {0, 0, 0, 7, 292, 0, 448, 73, 0, 0, 448, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    constexpr uint16_t m5[21] = {0, 0, 448, 0, 292, 7, 0, 0, 0, 73, 0, 0, 0, 295, 0, 0, 0, 0, 0, 0, 0};
+    constexpr uint16_t m6[21] = {256, 0, 0, 448, 0, 0, 292, 0, 0, 7, 0, 0, 0, 0, 0, 73, 0, 0, 0, 0, 0};
+    constexpr uint16_t m7[21] = {0, 7, 4, 0, 73, 0, 0, 73, 7, 0, 0, 448, 448, 0, 292, 0, 0, 0, 484, 0, 0};
+    constexpr uint16_t m8[21] = {73, 448, 0, 7, 0, 0, 0, 7, 0, 292, 7, 0, 292, 73, 0, 0, 448, 0, 0, 448, 73};
+    return S == 1 ? m1[t] : S == 2 ? m2[t] : S == 3 ? m3[t] : S == 4 ? m4[t] : S == 5 ? m5[t] : S == 6 ? m6[t] : S == 7 ? m7[t] : m8[t];
+}
+__host__ __device__ constexpr bool cell_major(int S) { return S >= 4; }
+// head-feature row pitch (bf16 elements): the head conv's 8-B stores of a tile hit
+// distinct banks with 772 words at S = 8 and 776 words at S = 4
+__host__ __device__ constexpr int lin_pitch(int S) { return S == 4 ? 1552 : 1544; }
+// the first k-step of tile t whose tap is not skipped: its MFMA takes the bias
+__host__ __device__ constexpr int first_kstep(int S, int t) {
+    int tap = 0;
+    while ((tap_skip(S, t) >> tap) & 1) ++tap;   // the centre tap is always on the board
+    return 2 * tap;
 }
 
 // Work split: a conv layer is NPT position tiles x CT co tiles = NPT*CT
@@ -209,26 +270,67 @@ struct Geo {
     }
 };
 
-template <int W, int CT, int NPT>
-__device__ __forceinline__ void make_geo(int lane, Geo<Plan<W, CT, NPT>::NT> &g) {
+// LDS row p of a group of S positions -> (position s, cell, order index idx)
+struct RowCell {
+    int s, cell, idx;   // cell < 0: a padding row past S * 42
+};
+template <int S>
+__device__ __forceinline__ RowCell row_cell(const uint8_t *smem, int p) {
+    if (p >= S * c4::kCells) return RowCell{0, -1, 0};
+    if constexpr (!cell_major(S)) {
+        const int s = p / c4::kCells, cell = p - s * c4::kCells;
+        return RowCell{s, cell, cell};
+    } else {
+        const int idx = p / S;
+        return RowCell{p - idx * S, (int)((const uint32_t *)(smem + kTab))[idx * 4], idx};
+    }
+}
+
+template <int W, int CT, int NPT, int S>
+__device__ __forceinline__ void make_geo(const uint8_t *smem, int lane, Geo<Plan<W, CT, NPT>::NT> &g) {
     using PL = Plan<W, CT, NPT>;
     const int col = lane & 15, q = lane >> 4;
 #pragma unroll
     for (int t = 0; t < PL::NT; ++t) {
         const int p = PL::gpt(t) * 16 + col;
-        const int cell = p % c4::kCells;
-        const int h = cell / c4::kCols, w = cell - h * c4::kCols;
+        if constexpr (!cell_major(S)) {   // position-major rows: a tap is a contiguous shift
+            const int cell = p % c4::kCells;
+            const int h = cell / c4::kCols, w = cell - h * c4::kCols;
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-            const int dh = tap / 3 - 1, dw = tap % 3 - 1;
-            const int r = p + dh * c4::kCols + dw;
-            const bool ok = (unsigned)(h + dh) < (unsigned)c4::kRows && (unsigned)(w + dw) < (unsigned)c4::kCols;
-            const int full = r * 128 + ((q ^ (r & 7)) << 4);
-            // an out-of-board tap reads the zero block below the buffer at the same
-            // 16-B granule its row would use, so it never adds a bank conflict
-            const uint32_t v = (uint32_t)((ok ? full : (full & 255) - 256) + 256);
-            if (tap & 1) g.rel2[t][tap >> 1] |= v << 16;
-            else g.rel2[t][tap >> 1] = v;
+            for (int tap = 0; tap < 9; ++tap) {
+                const int dh = tap / 3 - 1, dw = tap % 3 - 1;
+                const int r = p + dh * c4::kCols + dw;
+                const bool ok = (unsigned)(h + dh) < (unsigned)c4::kRows && (unsigned)(w + dw) < (unsigned)c4::kCols;
+                const int full = r * 128 + ((q ^ (r & 7)) << 4);
+                // an out-of-board tap reads the zero block below the buffer at the same
+                // 16-B granule its row would use, so it never adds a bank conflict
+                const uint32_t v = (uint32_t)((ok ? full : (full & 255) - 256) + 256);
+                if (tap & 1) g.rel2[t][tap >> 1] |= v << 16;
+                else g.rel2[t][tap >> 1] = v;
+            }
+        } else {   // cell-major rows through the staged table {cell, neighbour row groups}
+            const bool real = p < S * c4::kCells;
+            const int idx = real ? p / S : 0, s = p - idx * S;
+            const uint4 e = *(const uint4 *)(smem + kTab + idx * 16);
+            const int own = p * 128 + ((q ^ (p & 7)) << 4);
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const uint32_t word = tap < 4 ? e.y : tap < 8 ? e.z : e.w;
+                const int nb = (int)((word >> (8 * (tap & 3))) & 255u);
+                int v;
+                if (real && nb != 255) {   // the neighbour cell's row for this position
+                    const int r = nb * S + s;
+                    v = r * 128 + ((q ^ (r & 7)) << 4) + 256;
+                } else if (S == 4) {       // the zero block, at the granule an on-board neighbour of this
+                                           // colour would use (row group parity = checkerboard colour)
+                    const int r = (((idx ^ (tap / 3 + tap % 3)) & 1) << 2) + s;
+                    v = (r * 128 + ((q ^ (r & 7)) << 4)) & 255;
+                } else {                   // the zero block, at this row's own granule
+                    v = own & 255;
+                }
+                if (tap & 1) g.rel2[t][tap >> 1] |= (uint32_t)v << 16;
+                else g.rel2[t][tap >> 1] = (uint32_t)v;
+            }
         }
         g.epi[t] = p * 128 + ((((q >> 1)) ^ (p & 7)) << 4) + ((q & 1) << 3);
     }
@@ -258,7 +360,7 @@ __host__ __device__ constexpr int b_depth(int S) { return S <= 2 ? 4 : S <= 3 ? 
 // weights without a cold start.  `wn` is always a valid layer (the current one
 // when nothing follows): an unconditional prefetch keeps the vmcnt bookkeeping
 // free of branches.
-template <int W, int CT, int NPT, int IN, int DA, int DB>
+template <int W, int CT, int NPT, int S, int IN, int DA, int DB>
 __device__ __forceinline__ void conv_mfma(const uint8_t *smem, const Geo<Plan<W, CT, NPT>::NT> &g, const float *bias,
                                           const uint4 *__restrict__ w, const uint4 *__restrict__ wn, int lane,
                                           uint4 (&A)[DA][Plan<W, CT, NPT>::CTL],
@@ -275,12 +377,16 @@ __device__ __forceinline__ void conv_mfma(const uint8_t *smem, const Geo<Plan<W,
     }
     const uint4 *wl = w + PL::C0 * 64 + lane;
     const uint4 *wnl = wn + PL::C0 * 64 + lane;
+    // (tile, tap) pairs whose rows are all off the board for that tap are skipped
+    // (tap_skip); the indices below are compile-time constants once unrolled
+    auto live = [](int t, int ks) { return !((tap_skip(S, PL::gpt(t)) >> (ks >> 1)) & 1); };
     uint4 B[DB][NT];
 #pragma unroll
     for (int kb = 0; kb < DB - 1; ++kb) {
         const int tap = kb >> 1, flip = (kb & 1) << 6;
 #pragma unroll
-        for (int t = 0; t < NT; ++t) B[kb][t] = *(const uint4 *)(smem + (IN - 256) + (g.b(t, tap) ^ flip));
+        for (int t = 0; t < NT; ++t)
+            if (live(t, kb)) B[kb][t] = *(const uint4 *)(smem + (IN - 256) + (g.b(t, tap) ^ flip));
     }
 #pragma unroll
     for (int ks = 0; ks < kKStepsRes; ++ks) {
@@ -303,25 +409,38 @@ __device__ __forceinline__ void conv_mfma(const uint8_t *smem, const Geo<Plan<W,
             for (int c = 0; c < CTL; ++c) A[(ks + la) % DA][c] = wnl[((ks + la - kKStepsRes) * CT + c) * 64];
 #endif
         }
+        int nr = 0;   // B reads issued this k-step (for the issue-order hints)
         if (ks + lb < kKStepsRes) {
             const int tap = (ks + lb) >> 1, flip = ((ks + lb) & 1) << 6;
 #pragma unroll
             for (int t = 0; t < NT; ++t)
-                B[(ks + lb) % DB][t] = *(const uint4 *)(smem + (IN - 256) + (g.b(t, tap) ^ flip));
+                if (live(t, ks + lb)) {
+                    B[(ks + lb) % DB][t] = *(const uint4 *)(smem + (IN - 256) + (g.b(t, tap) ^ flip));
+                    ++nr;
+                }
         }
+        int nm = 0;
 #pragma unroll
         for (int i = 0; i < PL::n; ++i)
-            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[ks % DA][PL::co(i) - PL::C0]),
-                                                            as_bf16x8(B[ks % DB][PL::pt(i)]),
-                                                            ks == 0 ? bv[PL::co(i) - PL::C0] : acc[i], 0, 0, 0);
+            if (live(PL::pt(i), ks)) {
+                const int t = PL::gpt(PL::pt(i));
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[ks % DA][PL::co(i) - PL::C0]),
+                                                                as_bf16x8(B[ks % DB][PL::pt(i)]),
+                                                                ks == first_kstep(S, t) ? bv[PL::co(i) - PL::C0]
+                                                                                        : acc[i], 0, 0, 0);
+                ++nm;
+            }
         // issue order for this k-step: each MFMA followed by up to 2 VALU, one
         // LDS read (next B) and one weight load (A, DA-1 ahead)
+        const int ng = nm > nr ? nm : nr;
 #pragma unroll
         for (int i = 0; i < PL::n; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-            if (i < NT) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            if (i < CTL) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            if (i < ng) {
+                if (i < nm) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                if (i < nr) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                if (i < CTL) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -403,9 +522,10 @@ __device__ __forceinline__ void residual_mfma(const uint8_t *smem, const Geo<Pla
 // hold at bit col*7+row the value of that cell's (dh,dw) neighbour, so lane
 // element j of a position is bit (col*7+row) of N[s][8q+j].  FROM_X path
 // (Net::forward on arbitrary inputs): gather the fp32 input tensor.
-template <int W, int NPT, bool FROM_X>
+template <int W, int S, bool FROM_X>
 __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const float *__restrict__ x, int base_slot,
                                      int valid, int lane) {
+    constexpr int NPT = npt_of(S);
     using PL = Plan<W, 4, NPT>;
     constexpr int NT = PL::NT;
     const int col = lane & 15, q = lane >> 4;
@@ -415,12 +535,15 @@ __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const fl
     uint4 bv[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        const int p = PL::gpt(t) * 16 + col;
-        const int s = p / c4::kCells, cell = p - s * c4::kCells;
+        const RowCell rc = row_cell<S>(smem, PL::gpt(t) * 16 + col);
+        const int s = rc.s, cell = rc.cell < 0 ? 0 : rc.cell;   // padding rows: zero inputs (below)
         const int h = cell / c4::kCols, wc = cell - h * c4::kCols;
         uint16_t e[8];
-        if (!FROM_X) {
-            const uint4 *np = (const uint4 *)(smem + kPlanes) + s * 16 + q * 4;   // N[s][8q .. 8q+7]
+        if (rc.cell < 0) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) e[j] = 0;
+        } else if (!FROM_X) {
+            const uint4 *np = (const uint4 *)(smem + kPlanes) + s * (kPlaneRow / 2) + q * 4;   // N[s][8q .. 8q+7]
             const int b = wc * 7 + h;
 #pragma unroll
             for (int j2 = 0; j2 < 4; ++j2) {
@@ -459,7 +582,7 @@ __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const fl
         acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[PL::co(i)]), as_bf16x8(bv[PL::pt(i)]),
                                                         b4[PL::co(i)], 0, 0, 0);
     Geo<NT> g;
-    make_geo<W, 4, NPT>(lane, g);
+    make_geo<W, 4, NPT, S>(smem, lane, g);
     epilogue_act<W, NPT, kX, false>(smem, g, acc);
 }
 
@@ -480,12 +603,12 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
     constexpr int NPT = npt_of(S);
     using PL = Plan<W, kHeadCT, NPT>;
     Geo<PL::NT> g;
-    make_geo<W, kHeadCT, NPT>(lane, g);
+    make_geo<W, kHeadCT, NPT, S>(smem, lane, g);
     f32x4 acc[PL::n];
     constexpr int DA = a_depth(S), DB = b_depth(S);
     uint4 A[DA][PL::CTL];
     load_a_first<kHeadCT, PL::C0, PL::CTL, DA>(P.w_head, lane, A);
-    conv_mfma<W, kHeadCT, NPT, kX, DA, DB>(smem, g, (const float *)(smem + kBias) + kHid * (1 + 2 * P.blocks), P.w_head, P.w_head,
+    conv_mfma<W, kHeadCT, NPT, S, kX, DA, DB>(smem, g, (const float *)(smem + kBias) + kHid * (1 + 2 * P.blocks), P.w_head, P.w_head,
                               lane, A, acc);
 #ifdef SPAI_DIAG
     if (kDiagHead) {
@@ -499,15 +622,14 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
 #pragma unroll
     for (int i = 0; i < PL::n; ++i) {
         const int co0 = PL::co(i) * 16 + 4 * q;   // pad channels (zero weights and bias) come out as 0
-        const int p = PL::gpt(PL::pt(i)) * 16 + col;
-        const int s = p / c4::kCells, cell = p - s * c4::kCells;
-        if (co0 < kHC && (NPT * 16 == S * c4::kCells || s < S))
-            *(uint2 *)(H + s * kLinPitch + cell * kHC + co0) =
+        const RowCell rc = row_cell<S>(smem, PL::gpt(PL::pt(i)) * 16 + col);
+        if (co0 < kHC && rc.cell >= 0)   // H[s][cell * 36 + c] whatever the row order: the linear sums the same K order
+            *(uint2 *)(H + rc.s * lin_pitch(S) + rc.cell * kHC + co0) =
                 make_uint2(pack_relu_bf16x2(acc[i][0], acc[i][1]), pack_relu_bf16x2(acc[i][2], acc[i][3]));
     }
     // K padding [1512, 1536) of each row: 6 words of 8 B
     if (W == 0 && lane < S * 6)
-        *(uint2 *)(H + (lane / 6) * kLinPitch + kLinFeat + 4 * (lane % 6)) = make_uint2(0u, 0u);
+        *(uint2 *)(H + (lane / 6) * lin_pitch(S) + kLinFeat + 4 * (lane % 6)) = make_uint2(0u, 0u);
 #ifdef SPAI_DIAG
     if (kDiagHead) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -526,7 +648,7 @@ __device__ __forceinline__ void linear_mfma(uint8_t *smem, const uint4 (&wl)[kLi
     constexpr int k0 = kLinPerWave * W;
     constexpr int k1 = (kLinPerWave * (W + 1) < kLinKSteps) ? kLinPerWave * (W + 1) : kLinKSteps;
     const int s = lane & 15, q = lane >> 4;
-    const uint8_t *hrow = s < S ? smem + kH + s * kLinPitch * 2 + q * 16 : smem + kZ + q * 16;
+    const uint8_t *hrow = s < S ? smem + kH + s * lin_pitch(S) * 2 + q * 16 : smem + kZ + q * 16;
     const int hstep = s < S ? 64 : 0;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -552,9 +674,9 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
     constexpr int DA = a_depth(S), DB = b_depth(S);
     uint4 A[DA][PL4::CTL];
     if (P.blocks > 0) load_a_first<4, PL4::C0, PL4::CTL, DA>(P.w_res, lane, A);
-    stem<W, NPT, FROM_X>(smem, P, x, base, valid, lane);
+    stem<W, S, FROM_X>(smem, P, x, base, valid, lane);
     Geo<Plan<W, 4, NPT>::NT> g;
-    make_geo<W, 4, NPT>(lane, g);
+    make_geo<W, 4, NPT, S>(smem, lane, g);
     __syncthreads();
     stamp(P, W, lane, 1);
 #ifdef SPAI_C4_BLOCK_UNROLL
@@ -563,7 +685,7 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
     for (int b = 0; b < P.blocks; ++b) {   // relu(x + BN(conv(relu(BN(conv(x)))))), model/mod.rs:152-165
         f32x4 acc[Plan<W, 4, NPT>::n];
         const int l1 = 2 * b, l2 = 2 * b + 1;
-        conv_mfma<W, 4, NPT, kX, DA, DB>(smem, g, bias + kHid * (1 + l1), P.w_res + l1 * kLayer, P.w_res + l2 * kLayer, lane, A, acc);
+        conv_mfma<W, 4, NPT, S, kX, DA, DB>(smem, g, bias + kHid * (1 + l1), P.w_res + l1 * kLayer, P.w_res + l2 * kLayer, lane, A, acc);
 #ifdef SPAI_DIAG
         if (b == 0 && !kDiagHead) {   // make the k-loop's results visible before the stamp
             asm volatile("" ::"v"(acc[0][0]), "v"(acc[PL4::n - 1][3]));
@@ -582,7 +704,7 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
         if (b == 0 && !kDiagHead) stamp(P, W, lane, 19);
 #endif
         if (l1 < 12) stamp(P, W, lane, 2 + l1);
-        conv_mfma<W, 4, NPT, kY, DA, DB>(smem, g, bias + kHid * (1 + l2), P.w_res + l2 * kLayer,
+        conv_mfma<W, 4, NPT, S, kY, DA, DB>(smem, g, bias + kHid * (1 + l2), P.w_res + l2 * kLayer,
                             b + 1 < P.blocks ? P.w_res + (l2 + 1) * kLayer : P.w_res + l2 * kLayer, lane, A, acc);
         if (SPAI_RES_MFMA) {
             residual_mfma<W, NPT, kX>(smem, g, lane, acc);
@@ -650,6 +772,8 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
     if (tid < 64) ((uint32_t *)(smem + kZ))[tid] = 0u;
     else if (tid < 128) ((uint32_t *)(smem + kZ1))[tid - 64] = 0u;
     ((uint4 *)(smem + kWStem))[tid] = P.w_stem[tid];   // 256 x 16 B
+    if (tid < c4::kCells)   // this launch's geometry table (read after the group loop's first barrier)
+        ((uint4 *)(smem + kTab))[tid] = P.geo[S * c4::kCells + tid];
     {
         float *bias = (float *)(smem + kBias);
         const int nres = 2 * P.blocks * kHid;
@@ -678,7 +802,7 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
                 const int off = (tap % 3 - 1) * 7 + (tap / 3 - 1);
                 v = off >= 0 ? plane >> off : plane << -off;
             }
-            ((uint64_t *)(smem + kPlanes))[s * 32 + k] = v;
+            ((uint64_t *)(smem + kPlanes))[s * kPlaneRow + k] = v;
         }
         __syncthreads();
         stamp(P, wave, lane, 0);
@@ -918,6 +1042,24 @@ int net_create(spai_engine *e, int blocks, int hidden, const float *params, size
                 wlin[((size_t)ks * 64 + l) * 8 + j] = f2bf(v);
             }
     up(n->w_lin, wlin);
+    // geometry table: per S and row group idx, the cell and each tap's neighbour row group
+    std::vector<uint32_t> geo((size_t)9 * c4::kCells * 4, 0);
+    for (int S = 1; S <= kS; ++S) {
+        int idx_of[c4::kCells];
+        for (int i = 0; i < c4::kCells; ++i) idx_of[kCellOrder[S][i]] = i;
+        for (int i = 0; i < c4::kCells; ++i) {
+            const int cell = kCellOrder[S][i], h = cell / c4::kCols, w = cell % c4::kCols;
+            uint32_t *e = &geo[((size_t)S * c4::kCells + i) * 4];
+            e[0] = (uint32_t)cell;
+            for (int tap = 0; tap < 9; ++tap) {
+                const int hh = h + tap / 3 - 1, ww = w + tap % 3 - 1;
+                const bool ok = hh >= 0 && hh < c4::kRows && ww >= 0 && ww < c4::kCols;
+                const uint32_t nb = ok ? (uint32_t)idx_of[hh * c4::kCols + ww] : 255u;
+                e[1 + tap / 4] |= nb << (8 * (tap % 4));
+            }
+        }
+    }
+    up(n->geo, geo);
     up(n->b_pol, std::vector<float>(pol_b, pol_b + 7));
     up(n->b_val, std::vector<float>(val_b, val_b + 1));
     if (rc != SPAI_OK) {
@@ -937,6 +1079,7 @@ void net_destroy(spai_net *n) {
     n->io_mine.release();
     n->io_theirs.release();
     n->io_count.release();
+    n->geo.release();
     delete n;
 }
 
@@ -951,6 +1094,7 @@ static NetParams params_of(const spai_net *n) {
     P.w_lin = (const uint4 *)n->w_lin.p;
     P.b_pol = n->b_pol.p;
     P.b_val = n->b_val.p;
+    P.geo = (const uint4 *)n->geo.p;
     P.stamps = nullptr;
     P.blocks = n->blocks;
     return P;

@@ -127,6 +127,7 @@ struct spai_net {
     spai::DevBuf<float> io_x, io_logits, io_value, io_priors;   // scratch for forward/predict calls
     spai::DevBuf<uint64_t> io_mine, io_theirs;
     spai::DevBuf<uint32_t> io_count;
+    spai::DevBuf<uint32_t> geo;     // LDS row -> cell / neighbour table of the cell orders (net_c4.hip)
 };
 
 // Device training step of the C4 net (learner.hip).

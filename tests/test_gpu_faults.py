@@ -71,3 +71,18 @@ def test_chess_nan_value_reports_nan(spai):
     assert ex.value.code == -5
     net.close()
     e.close()
+
+
+def test_c4_zero_searches_on_a_fresh_engine(spai):
+    """num_searches = 0 on a fresh engine (the per-iteration counters
+    were not allocated, and the memset of a null buffer failed): the search returns
+    with no children, and the root policy is Policy::normalize of all-zero visits,
+    0/0 = NaN as in the reference (mcts.rs:310-331 with an unexpanded root)"""
+    e = spai.Engine(num_searches=4, max_trees=8, eval_kind=spai.EVAL_HASH, seed=2)
+    e.trees_create(8)
+    pol, ids, vis, nc = e.search(np.arange(8), 0)
+    assert np.all(nc == 0) and np.all(vis == 0)
+    assert np.all(np.isnan(pol))
+    pol, ids, vis, nc = e.search(np.arange(8), 4)   # the engine still searches afterwards
+    assert np.all(nc == 7) and np.all(vis.sum(1) == 3)
+    e.close()
