@@ -77,7 +77,7 @@ constexpr int kPlanes = kBias + kBiasFloats * 4;   // stem neighbour planes [8][
                                                    // in different 16-B bank groups)
 constexpr int kPlaneRow = 34;
 constexpr int kWStem = kPlanes + kS * kPlaneRow * 8;   // stem weight fragments [4 ct][64 lanes] x 16 B, staged once
-constexpr int kTab = kWStem + 4 * 64 * 16;         // the launch's geometry table: [42 row groups] x 16 B (NetParams::geo)
+constexpr int kTab = kWStem + 4 * 64 * 16;         // k_geo_init: one S's row-group table [42] x 16 B (NetParams::geo)
 constexpr int kLdsBytes = kTab + 42 * 16;
 constexpr int kStamps = 24;                // phase stamps per wave in the diagnostic mode (17..19: inside block 0 conv1;
                                            // 20/21: s_memtime / s_memrealtime at kernel entry, 22: s_memrealtime at the
@@ -98,6 +98,7 @@ struct NetParams {
     // per group size S and row group idx (= LDS row / S): {cell, then the row group
     // holding each 3x3 tap's neighbour cell as 9 bytes (0xFF off the board)} x 16 B
     const uint4 *geo;             // [9][42]
+    const uint4 *lane_geo;        // per-lane geometry of every (S, plan, wave, tile): lane_geo_at, k_geo_init
     unsigned long long *stamps;   // diagnostic: [grid][4 waves][kStamps] s_memtime, or null
     int blocks;
 };
@@ -336,6 +337,92 @@ __device__ __forceinline__ void make_geo(const uint8_t *smem, int lane, Geo<Plan
     }
 }
 
+// Per-lane geometry table (NetParams::lane_geo), built once per net by
+// k_geo_init from make_geo: computing it in the forward cost ~10 VALU per
+// (tile, tap), some 900 cycles per position tile per plan before the first MFMA.
+// Entry (S, plan, W, t) holds 64 lanes x 32 B: {rel2[5], epi, aux, 0}.  Plan 0 =
+// the 64-channel layers (CT = 4), whose aux feeds the stem: s | (bit col*7+row)
+// << 8 (padding rows: s = S, a zeroed plane row); plan 1 = the head conv (CT = 3),
+// whose aux is the head-feature offset s * lin_pitch(S) + cell * 36, -1 on padding.
+constexpr int kGeoNT = 8;   // the most position tiles a wave holds (S = 3, co-major)
+__host__ __device__ constexpr size_t lane_geo_at(int S, int plan, int W, int t) {
+    return ((((size_t)(S - 1) * 2 + plan) * kWaves + W) * kGeoNT + t) * 64 * 2;   // in uint4
+}
+constexpr size_t kLaneGeoU4 = lane_geo_at(kS + 1, 0, 0, 0);
+
+template <int W, int CT, int NPT, int S>
+__device__ __forceinline__ void load_geo(const NetParams &P, int lane, Geo<Plan<W, CT, NPT>::NT> &g,
+                                         int (&aux)[Plan<W, CT, NPT>::NT]) {
+    constexpr int NT = Plan<W, CT, NPT>::NT;
+    static_assert(NT <= kGeoNT, "lane geometry table depth");
+    const uint4 *src = P.lane_geo + lane_geo_at(S, CT == 3, W, 0) + 2 * lane;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const uint4 a = src[t * 128], b = src[t * 128 + 1];
+        g.rel2[t][0] = a.x;
+        g.rel2[t][1] = a.y;
+        g.rel2[t][2] = a.z;
+        g.rel2[t][3] = a.w;
+        g.rel2[t][4] = b.x;
+        g.epi[t] = (int)b.y;
+        aux[t] = (int)b.z;
+    }
+}
+
+template <int S, int CT, int W>
+__device__ void geo_init_one(const uint8_t *smem, uint4 *out, int lane) {
+    constexpr int NPT = npt_of(S);
+    using PL = Plan<W, CT, NPT>;
+    Geo<PL::NT> g;
+    make_geo<W, CT, NPT, S>(smem, lane, g);
+    uint4 *dst = out + lane_geo_at(S, CT == 3, W, 0) + 2 * lane;
+    for (int t = 0; t < PL::NT; ++t) {
+        const RowCell rc = row_cell<S>(smem, PL::gpt(t) * 16 + (lane & 15));
+        int aux;
+        if (CT == 4) {
+            const int h = rc.cell / c4::kCols, w = rc.cell - h * c4::kCols;
+            aux = rc.cell < 0 ? S : rc.s | (w * 7 + h) << 8;
+        } else {
+            aux = rc.cell < 0 ? -1 : rc.s * lin_pitch(S) + rc.cell * kHC;
+        }
+        dst[t * 128] = make_uint4(g.rel2[t][0], g.rel2[t][1], g.rel2[t][2], g.rel2[t][3]);
+        dst[t * 128 + 1] = make_uint4(g.rel2[t][4], (uint32_t)g.epi[t], (uint32_t)aux, 0u);
+    }
+}
+
+template <int S>
+__device__ void geo_init_s(const uint8_t *smem, uint4 *out, int plan, int W, int lane) {
+    if (plan == 0) {
+        if (W == 0) geo_init_one<S, 4, 0>(smem, out, lane);
+        else if (W == 1) geo_init_one<S, 4, 1>(smem, out, lane);
+        else if (W == 2) geo_init_one<S, 4, 2>(smem, out, lane);
+        else geo_init_one<S, 4, 3>(smem, out, lane);
+    } else {
+        if (W == 0) geo_init_one<S, 3, 0>(smem, out, lane);
+        else if (W == 1) geo_init_one<S, 3, 1>(smem, out, lane);
+        else if (W == 2) geo_init_one<S, 3, 2>(smem, out, lane);
+        else geo_init_one<S, 3, 3>(smem, out, lane);
+    }
+}
+
+// one 64-thread workgroup per (S, plan, wave): blockIdx.x = ((S - 1) * 2 + plan) * 4 + W
+__global__ __launch_bounds__(64) void k_geo_init(const uint4 *__restrict__ geo, uint4 *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
+    const int S = blockIdx.x / 8 + 1, plan = (blockIdx.x / 4) & 1, W = blockIdx.x & 3, lane = threadIdx.x;
+    if (lane < c4::kCells) ((uint4 *)(smem + kTab))[lane] = geo[S * c4::kCells + lane];
+    __syncthreads();
+    switch (S) {
+    case 1: geo_init_s<1>(smem, out, plan, W, lane); break;
+    case 2: geo_init_s<2>(smem, out, plan, W, lane); break;
+    case 3: geo_init_s<3>(smem, out, plan, W, lane); break;
+    case 4: geo_init_s<4>(smem, out, plan, W, lane); break;
+    case 5: geo_init_s<5>(smem, out, plan, W, lane); break;
+    case 6: geo_init_s<6>(smem, out, plan, W, lane); break;
+    case 7: geo_init_s<7>(smem, out, plan, W, lane); break;
+    default: geo_init_s<8>(smem, out, plan, W, lane); break;
+    }
+}
+
 // Prefetch depths per group size: a small group has few MFMAs per k-step to
 // hide a weight load (L2) or an LDS read behind, but registers to spare.
 // (DA must divide the 18 k-steps of a layer: the ring carries the next layer's
@@ -524,27 +611,22 @@ __device__ __forceinline__ void residual_mfma(const uint8_t *smem, const Geo<Pla
 // (Net::forward on arbitrary inputs): gather the fp32 input tensor.
 template <int W, int S, bool FROM_X>
 __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const float *__restrict__ x, int base_slot,
-                                     int valid, int lane) {
+                                     int valid, int lane, const Geo<Plan<W, 4, npt_of(S)>::NT> &g,
+                                     const int (&aux)[Plan<W, 4, npt_of(S)>::NT]) {
     constexpr int NPT = npt_of(S);
     using PL = Plan<W, 4, NPT>;
     constexpr int NT = PL::NT;
-    const int col = lane & 15, q = lane >> 4;
+    const int q = lane >> 4;
     uint4 a[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) a[c] = ((const uint4 *)(smem + kWStem))[c * 64 + lane];
     uint4 bv[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-        const RowCell rc = row_cell<S>(smem, PL::gpt(t) * 16 + col);
-        const int s = rc.s, cell = rc.cell < 0 ? 0 : rc.cell;   // padding rows: zero inputs (below)
-        const int h = cell / c4::kCols, wc = cell - h * c4::kCols;
+        const int s = aux[t] & 255, b = aux[t] >> 8;   // b = col*7 + row of the row's cell
         uint16_t e[8];
-        if (rc.cell < 0) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) e[j] = 0;
-        } else if (!FROM_X) {
+        if (!FROM_X) {
             const uint4 *np = (const uint4 *)(smem + kPlanes) + s * (kPlaneRow / 2) + q * 4;   // N[s][8q .. 8q+7]
-            const int b = wc * 7 + h;
 #pragma unroll
             for (int j2 = 0; j2 < 4; ++j2) {
                 const uint4 w4 = np[j2];
@@ -553,6 +635,7 @@ __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const fl
                 e[2 * j2 + 1] = ((n1 >> b) & 1ull) ? 0x3F80u : 0u;
             }
         } else {
+            const int h = b % c4::kCols, wc = b / c4::kCols;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int kk = 8 * q + j;
@@ -581,8 +664,6 @@ __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const fl
     for (int i = 0; i < PL::n; ++i)
         acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[PL::co(i)]), as_bf16x8(bv[PL::pt(i)]),
                                                         b4[PL::co(i)], 0, 0, 0);
-    Geo<NT> g;
-    make_geo<W, 4, NPT, S>(smem, lane, g);
     epilogue_act<W, NPT, kX, false>(smem, g, acc);
 }
 
@@ -603,11 +684,14 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
     constexpr int NPT = npt_of(S);
     using PL = Plan<W, kHeadCT, NPT>;
     Geo<PL::NT> g;
-    make_geo<W, kHeadCT, NPT, S>(smem, lane, g);
+    int hoff[PL::NT];   // head-feature offset of each tile's row (-1: padding)
+    load_geo<W, kHeadCT, NPT, S>(P, lane, g, hoff);
     f32x4 acc[PL::n];
     constexpr int DA = a_depth(S), DB = b_depth(S);
     uint4 A[DA][PL::CTL];
     load_a_first<kHeadCT, PL::C0, PL::CTL, DA>(P.w_head, lane, A);
+    // the linear's weights after the conv's first fragments: the loads return in order
+    if (!SPAI_LIN_LATE) load_lin<W>(P, lane, wl);
     conv_mfma<W, kHeadCT, NPT, S, kX, DA, DB>(smem, g, (const float *)(smem + kBias) + kHid * (1 + 2 * P.blocks), P.w_head, P.w_head,
                               lane, A, acc);
 #ifdef SPAI_DIAG
@@ -617,14 +701,14 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
     }
 #endif
     if (SPAI_LIN_LATE) load_lin<W>(P, lane, wl);
-    const int col = lane & 15, q = lane >> 4;
+    const int q = lane >> 4;
     uint16_t *H = (uint16_t *)(smem + kH);
 #pragma unroll
     for (int i = 0; i < PL::n; ++i) {
         const int co0 = PL::co(i) * 16 + 4 * q;   // pad channels (zero weights and bias) come out as 0
-        const RowCell rc = row_cell<S>(smem, PL::gpt(PL::pt(i)) * 16 + col);
-        if (co0 < kHC && rc.cell >= 0)   // H[s][cell * 36 + c] whatever the row order: the linear sums the same K order
-            *(uint2 *)(H + rc.s * lin_pitch(S) + rc.cell * kHC + co0) =
+        const int off = hoff[PL::pt(i)];
+        if (co0 < kHC && off >= 0)   // H[s][cell * 36 + c] whatever the row order: the linear sums the same K order
+            *(uint2 *)(H + off + co0) =
                 make_uint2(pack_relu_bf16x2(acc[i][0], acc[i][1]), pack_relu_bf16x2(acc[i][2], acc[i][3]));
     }
     // K padding [1512, 1536) of each row: 6 words of 8 B
@@ -641,7 +725,7 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
 // fused policy|value linear on MFMA: out[s][o] = sum_k H[s][k] * Wl[o][k]
 // (o < 7 policy logits over k < 1344, o = 7 value pre-activation over
 // 1344 <= k < 1470; connect_four.rs:63-64,69-70).  Wave W takes k-steps
-// [12W, 12W+12) of 46 (weights prefetched by load_lin before the head conv);
+// [12W, 12W+12) of 48 (weights loaded by load_lin behind the head conv's first fragments);
 // partial sums go to LDS.
 template <int W, int S>
 __device__ __forceinline__ void linear_mfma(uint8_t *smem, const uint4 (&wl)[kLinPerWave], int lane) {
@@ -666,7 +750,8 @@ __device__ __forceinline__ void linear_mfma(uint8_t *smem, const uint4 (&wl)[kLi
 
 template <int W, int S, bool FROM_X>
 __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &P, const float *__restrict__ x,
-                                                int base, int valid, int lane) {
+                                                int base, int valid, int lane, const Geo<Plan<W, 4, npt_of(S)>::NT> &g,
+                                                const int (&aux)[Plan<W, 4, npt_of(S)>::NT]) {
     constexpr int NPT = npt_of(S);
     using PL4 = Plan<W, 4, NPT>;
     constexpr size_t kLayer = (size_t)kKStepsRes * 4 * 64;
@@ -674,9 +759,7 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
     constexpr int DA = a_depth(S), DB = b_depth(S);
     uint4 A[DA][PL4::CTL];
     if (P.blocks > 0) load_a_first<4, PL4::C0, PL4::CTL, DA>(P.w_res, lane, A);
-    stem<W, S, FROM_X>(smem, P, x, base, valid, lane);
-    Geo<Plan<W, 4, NPT>::NT> g;
-    make_geo<W, 4, NPT, S>(smem, lane, g);
+    stem<W, S, FROM_X>(smem, P, x, base, valid, lane, g, aux);
     __syncthreads();
     stamp(P, W, lane, 1);
 #ifdef SPAI_C4_BLOCK_UNROLL
@@ -717,22 +800,10 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
     }
     uint4 wl[kLinPerWave];
     if (kDiagHead) stamp(P, W, lane, 19);   // diagnostic head mode: 19 = before the head, 17 = head k-loop, 18 = H written
-    if (!SPAI_LIN_LATE) load_lin<W>(P, lane, wl);
     head_layer<W, S>(smem, P, lane, wl);
     __syncthreads();
     stamp(P, W, lane, 14);
     linear_mfma<W, S>(smem, wl, lane);
-}
-
-template <int S, bool FROM_X>
-__device__ __forceinline__ void run_group(uint8_t *smem, const NetParams &P, const float *__restrict__ x, int base,
-                                          int valid, int wave, int lane) {
-    switch (wave) {
-    case 0: torso_and_heads<0, S, FROM_X>(smem, P, x, base, valid, lane); break;
-    case 1: torso_and_heads<1, S, FROM_X>(smem, P, x, base, valid, lane); break;
-    case 2: torso_and_heads<2, S, FROM_X>(smem, P, x, base, valid, lane); break;
-    default: torso_and_heads<3, S, FROM_X>(smem, P, x, base, valid, lane); break;
-    }
 }
 
 // Group size for `count` leaves on `grid` workgroups: the fewest rounds R of at
@@ -747,33 +818,18 @@ __host__ __device__ inline int group_size(uint32_t count, uint32_t grid) {
     return g < 1 ? 1 : g > kS ? kS : g;
 }
 
-// Persistent forward: the grid is at most one workgroup per CU; each workgroup
-// loops over groups of S positions (S from the device-side leaf count, see
-// group_size; FROM_X and the diagnostic mode use S = force_s).
-template <bool FROM_X>
-__global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict__ count_ptr, uint32_t count_imm,
-                                                      int force_s, const uint64_t *__restrict__ mine,
-                                                      const uint64_t *__restrict__ theirs, const float *__restrict__ x,
-                                                      NetParams P, float *__restrict__ priors,
-                                                      float *__restrict__ value, float *__restrict__ logits) {
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
-    stamp(P, threadIdx.x >> 6, threadIdx.x & 63, 20);
-    stamp_real(P, threadIdx.x >> 6, threadIdx.x & 63, 21);
-    const uint32_t count = count_ptr ? *count_ptr : count_imm;
-    const int S = force_s > 0 ? force_s : group_size(count, gridDim.x);
-    const int ngroups = (int)((count + S - 1) / S);
-    if ((int)blockIdx.x >= ngroups) return;
-    const int tid = threadIdx.x, lane = tid & 63;
-#ifdef SPAI_FWD_PRIO
-    __builtin_amdgcn_s_setprio(SPAI_FWD_PRIO);   // experiment: issue priority against co-resident tree kernels
-#endif
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-
+// The group loop of one (wave, group size) variant.
+template <int W, int S, bool FROM_X>
+__device__ __forceinline__ void run_groups(uint8_t *smem, const NetParams &P, uint32_t count, int ngroups,
+                                           const uint64_t *__restrict__ mine, const uint64_t *__restrict__ theirs,
+                                           const float *__restrict__ x, float *__restrict__ priors,
+                                           float *__restrict__ value, float *__restrict__ logits, int tid) {
+    constexpr int wave = W;
+    const int lane = tid & 63;
+    // launch constants: the zero blocks, stem weights and every conv bias
     if (tid < 64) ((uint32_t *)(smem + kZ))[tid] = 0u;
     else if (tid < 128) ((uint32_t *)(smem + kZ1))[tid - 64] = 0u;
     ((uint4 *)(smem + kWStem))[tid] = P.w_stem[tid];   // 256 x 16 B
-    if (tid < c4::kCells)   // this launch's geometry table (read after the group loop's first barrier)
-        ((uint4 *)(smem + kTab))[tid] = P.geo[S * c4::kCells + tid];
     {
         float *bias = (float *)(smem + kBias);
         const int nres = 2 * P.blocks * kHid;
@@ -781,6 +837,16 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
             bias[i] = i < kHid ? P.b_stem[i] : i < kHid + nres ? P.b_res[i - kHid] : P.b_head[i - kHid - nres];
     }
     for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+        // hide the lane id from loop-invariant code motion: the trunk geometry (and
+        // every layer's per-lane addressing) hoisted out of the loop would stay live
+        // through the head, and the forward's register footprint decides whether the
+        // other search chain's tree kernels can run beside it (scripts/kernel_regs.py)
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        ln &= 63;   // restore the known range for the compiler
+        Geo<Plan<W, 4, npt_of(S)>::NT> g;
+        int aux[Plan<W, 4, npt_of(S)>::NT];
+        load_geo<W, 4, npt_of(S), S>(P, ln, g, aux);   // before the bitboard loads: the two latencies overlap
         const int base = grp * S;
         const int valid = min(S, (int)count - base);
         if (tid < kS) {
@@ -807,29 +873,7 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
         __syncthreads();
         stamp(P, wave, lane, 0);
         if (grp == (int)blockIdx.x) stamp_real(P, wave, lane, 22);
-        // hide the lane id from loop-invariant code motion: hoisting the per-lane
-        // geometry out of the group loop would keep it live across every layer
-        int ln = lane;
-        asm volatile("" : "+v"(ln));
-        ln &= 63;   // restore the known range for the compiler
-        if constexpr (FROM_X) {
-            run_group<kS, true>(smem, P, x, base, valid, wave, ln);
-        } else {
-#ifdef SPAI_ONLY_S
-            run_group<SPAI_ONLY_S, false>(smem, P, x, base, valid, wave, ln);
-#else
-            switch (S) {
-            case 1: run_group<1, false>(smem, P, x, base, valid, wave, ln); break;
-            case 2: run_group<2, false>(smem, P, x, base, valid, wave, ln); break;
-            case 3: run_group<3, false>(smem, P, x, base, valid, wave, ln); break;
-            case 4: run_group<4, false>(smem, P, x, base, valid, wave, ln); break;
-            case 5: run_group<5, false>(smem, P, x, base, valid, wave, ln); break;
-            case 6: run_group<6, false>(smem, P, x, base, valid, wave, ln); break;
-            case 7: run_group<7, false>(smem, P, x, base, valid, wave, ln); break;
-            default: run_group<8, false>(smem, P, x, base, valid, wave, ln); break;
-            }
-#endif
-        }
+        torso_and_heads<W, S, FROM_X>(smem, P, x, base, valid, ln, g, aux);
         __syncthreads();
         stamp(P, wave, lane, 15);
         if (tid < valid) {
@@ -873,7 +917,62 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
         stamp(P, wave, lane, 16);
         __syncthreads();   // kB / planes / L are rewritten by the next group
     }
-    stamp_real(P, wave, lane, 23);
+}
+
+template <int S, bool FROM_X>
+__device__ __forceinline__ void dispatch_wave(uint8_t *smem, const NetParams &P, uint32_t count, int ngroups,
+                                              const uint64_t *__restrict__ mine, const uint64_t *__restrict__ theirs,
+                                              const float *__restrict__ x, float *__restrict__ priors,
+                                              float *__restrict__ value, float *__restrict__ logits, int wave, int tid) {
+    switch (wave) {
+    case 0: run_groups<0, S, FROM_X>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
+    case 1: run_groups<1, S, FROM_X>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
+    case 2: run_groups<2, S, FROM_X>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
+    default: run_groups<3, S, FROM_X>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
+    }
+}
+
+// Persistent forward: the grid is at most one workgroup per CU; each workgroup
+// loops over groups of S positions (S from the device-side leaf count, see
+// group_size; FROM_X and the diagnostic mode use S = force_s).
+template <bool FROM_X>
+__global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict__ count_ptr, uint32_t count_imm,
+                                                      int force_s, const uint64_t *__restrict__ mine,
+                                                      const uint64_t *__restrict__ theirs, const float *__restrict__ x,
+                                                      NetParams P, float *__restrict__ priors,
+                                                      float *__restrict__ value, float *__restrict__ logits) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
+    stamp(P, threadIdx.x >> 6, threadIdx.x & 63, 20);
+    stamp_real(P, threadIdx.x >> 6, threadIdx.x & 63, 21);
+    const uint32_t count = count_ptr ? *count_ptr : count_imm;
+    const int S = force_s > 0 ? force_s : group_size(count, gridDim.x);
+    const int ngroups = (int)((count + S - 1) / S);
+    if ((int)blockIdx.x >= ngroups) return;
+    const int tid = threadIdx.x;
+#ifdef SPAI_FWD_PRIO
+    __builtin_amdgcn_s_setprio(SPAI_FWD_PRIO);   // experiment: issue priority against co-resident tree kernels
+#endif
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    if constexpr (FROM_X) {
+        dispatch_wave<kS, true>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid);
+    } else {
+#ifdef SPAI_ONLY_S
+        dispatch_wave<SPAI_ONLY_S, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid);
+#else
+        switch (S) {
+        case 1: dispatch_wave<1, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid); break;
+        case 2: dispatch_wave<2, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid); break;
+        case 3: dispatch_wave<3, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid); break;
+        case 4: dispatch_wave<4, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid); break;
+        case 5: dispatch_wave<5, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid); break;
+        case 6: dispatch_wave<6, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid); break;
+        case 7: dispatch_wave<7, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid); break;
+        default: dispatch_wave<8, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid); break;
+        }
+#endif
+    }
+    stamp_real(P, wave, tid & 63, 23);
 }
 
 // ---------------------------------------------------------------- host packing
@@ -1060,6 +1159,14 @@ int net_create(spai_engine *e, int blocks, int hidden, const float *params, size
         }
     }
     up(n->geo, geo);
+    if (rc == SPAI_OK) rc = n->lane_geo.alloc(kLaneGeoU4 * 4);
+    if (rc == SPAI_OK) {
+        k_geo_init<<<kS * 2 * kWaves, 64, 0, e->stream>>>((const uint4 *)n->geo.p, (uint4 *)n->lane_geo.p);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(e->stream) != hipSuccess) {
+            set_error("lane geometry kernel failed");
+            rc = SPAI_ERR_DEVICE;
+        }
+    }
     up(n->b_pol, std::vector<float>(pol_b, pol_b + 7));
     up(n->b_val, std::vector<float>(val_b, val_b + 1));
     if (rc != SPAI_OK) {
@@ -1080,6 +1187,7 @@ void net_destroy(spai_net *n) {
     n->io_theirs.release();
     n->io_count.release();
     n->geo.release();
+    n->lane_geo.release();
     delete n;
 }
 
@@ -1095,6 +1203,7 @@ static NetParams params_of(const spai_net *n) {
     P.b_pol = n->b_pol.p;
     P.b_val = n->b_val.p;
     P.geo = (const uint4 *)n->geo.p;
+    P.lane_geo = (const uint4 *)n->lane_geo.p;
     P.stamps = nullptr;
     P.blocks = n->blocks;
     return P;

@@ -128,6 +128,7 @@ struct spai_net {
     spai::DevBuf<uint64_t> io_mine, io_theirs;
     spai::DevBuf<uint32_t> io_count;
     spai::DevBuf<uint32_t> geo;     // LDS row -> cell / neighbour table of the cell orders (net_c4.hip)
+    spai::DevBuf<uint32_t> lane_geo;   // per-lane conv geometry of every (group size, plan, wave, tile) (net_c4.hip)
 };
 
 // Device training step of the C4 net (learner.hip).
