@@ -16,9 +16,11 @@ if [ -n "${PHASES:-}" ]; then   # per-phase stamps of the diagnostic build (make
   cat $O/phases.txt
 fi
 libs=$(for v in $VARS; do printf "build_exp/libspai_%s.so," $v; done)
-timeout -k 10 300 python scripts/fwd_sweep.py --libs ${libs%,} --counts ${COUNTS:-256,512,1006,1500,2048,4096} \
-    > $O/sweep.txt 2>&1 || { tail -5 $O/sweep.txt; exit 1; }
-cat $O/sweep.txt
+for sw in $(seq 1 ${SWEEPS:-2}); do   # the variants alternate: A B A B
+  timeout -k 10 300 python scripts/fwd_sweep.py --libs ${libs%,} --counts ${COUNTS:-256,512,1006,1500,2048,4096} \
+      > $O/sweep_$sw.txt 2>&1 || { tail -5 $O/sweep_$sw.txt; exit 1; }
+  cat $O/sweep_$sw.txt
+done | tee $O/sweep.txt || exit 1
 for r in $(seq 1 ${ROUNDS:-2}); do
   for v in $VARS; do
     SPAI_LIB=$PWD/build_exp/libspai_$v.so timeout -k 10 300 python bench.py --steps ${STEPS:-2} --warmup 1 --no-cpu-baseline \

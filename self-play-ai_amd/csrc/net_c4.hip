@@ -447,8 +447,101 @@ __host__ __device__ constexpr int b_depth(int S) { return S <= 2 ? 4 : S <= 3 ? 
 // weights without a cold start.  `wn` is always a valid layer (the current one
 // when nothing follows): an unconditional prefetch keeps the vmcnt bookkeeping
 // free of branches.
-template <int W, int CT, int NPT, int S, int IN, int DA, int DB>
-__device__ __forceinline__ void conv_mfma(const uint8_t *smem, const Geo<Plan<W, CT, NPT>::NT> &g, const float *bias,
+// The last tap of a 64-channel layer, task-major, with the epilogue fused
+// (conv_mfma EPI > 0): k-steps 16 and 17 of task i (and, EPI = 2, the residual
+// identity MFMA on the center-tap fragment of the block input at OUT), then
+// relu/bf16 of task i - 2 into OUT.
+template <int W, int CT, int NPT, int S, int DA, int DB, int EPI, int OUT>
+__device__ __forceinline__ void final_tap_epilogue(uint8_t *smem, const Geo<Plan<W, CT, NPT>::NT> &g, int lane,
+                                                   const uint4 (&A)[DA][Plan<W, CT, NPT>::CTL],
+                                                   const uint4 (&B)[DB][Plan<W, CT, NPT>::NT],
+                                                   const f32x4 (&bv)[Plan<W, CT, NPT>::CTL],
+                                                   f32x4 (&acc)[Plan<W, CT, NPT>::n]) {
+    using PL = Plan<W, CT, NPT>;
+    constexpr int n = PL::n, k0 = kKStepsRes - 2, D = 2;
+    static_assert(CT == 4, "fused epilogue: 64-channel layers");
+    auto live = [](int t, int ks) { return !((tap_skip(S, PL::gpt(t)) >> (ks >> 1)) & 1); };
+    uint4 id[2];   // residual identities (residual_mfma)
+    uint4 rb[3];   // residual B fragments, two tasks ahead
+    if (EPI == 2) {
+        const int m = lane & 15, q = lane >> 4;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int j = 16 * h + m - 8 * q;
+            uint32_t w[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w[e] = j == 2 * e ? 0x3F80u : j == 2 * e + 1 ? 0x3F800000u : 0u;
+            id[h] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+#pragma unroll
+        for (int i = 0; i < 2 && i < n; ++i)
+            rb[i] = *(const uint4 *)(smem + (OUT - 256) + (g.b(PL::pt(i), 4) ^ ((PL::co(i) >> 1) << 6)));
+    }
+#pragma unroll
+    for (int i = 0; i < n + D; ++i) {
+        int nm = 0, nv = 0, nw = 0, nrd = 0;
+        if (i < n) {
+            if (EPI == 2 && i + 2 < n) {
+                rb[(i + 2) % 3] = *(const uint4 *)(smem + (OUT - 256) + (g.b(PL::pt(i + 2), 4) ^ ((PL::co(i + 2) >> 1) << 6)));
+                ++nrd;
+            }
+            const int t = PL::gpt(PL::pt(i)), c = PL::co(i) - PL::C0;
+#pragma unroll
+            for (int ks = k0; ks < kKStepsRes; ++ks)
+                if (live(PL::pt(i), ks)) {
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[ks % DA][c]), as_bf16x8(B[ks % DB][PL::pt(i)]),
+                                                                    ks == first_kstep(S, t) ? bv[c] : acc[i], 0, 0, 0);
+                    ++nm;
+                }
+            if (EPI == 2) {
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(id[PL::co(i) & 1]), as_bf16x8(rb[i % 3]), acc[i],
+                                                                0, 0, 0);
+                ++nm;
+            }
+        }
+        if (i >= D) {
+            const int j = i - D;
+            const int off = OUT + (g.epi[PL::pt(j)] ^ (PL::co(j) << 5));
+            *(uint2 *)(smem + off) = make_uint2(pack_relu_bf16x2(acc[j][0], acc[j][1]), pack_relu_bf16x2(acc[j][2], acc[j][3]));
+            nv = 5;
+            nw = 1;
+        }
+        // issue order: the MFMAs with the epilogue's 5 VALU in their gaps, then the store and the read
+        if (nm >= 1) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            if (nv) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        }
+        if (nm >= 2) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            if (nv) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        }
+        if (nm >= 3) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            if (nv) __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        }
+        if (nv) {
+            if (nm == 0) __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+            else if (nm == 1) __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            else if (nm == 2) __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        }
+        if (nw) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        if (nrd) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+#ifndef SPAI_FUSE_EPI
+#define SPAI_FUSE_EPI 1
+#endif
+// EPI > 0 fuses the layer's epilogue into its last tap (k-steps 16 and 17): the
+// final tap runs task-major -- each task's two MFMAs back to back (EPI = 2: plus
+// the residual MFMA, see residual_mfma), and the ReLU/bf16 pack and LDS store of
+// task i - 2 ride in the MFMA gaps of task i instead of a serial epilogue after
+// the k-loop.  Safe to store while other waves still run this layer: OUT is not
+// this layer's input, and a residual read that meets another wave's fresh store
+// in the other 16 channels of its 32-channel block multiplies it by zero.
+template <int W, int CT, int NPT, int S, int IN, int DA, int DB, int EPI = 0, int OUT = 0>
+__device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, NPT>::NT> &g, const float *bias,
                                           const uint4 *__restrict__ w, const uint4 *__restrict__ wn, int lane,
                                           uint4 (&A)[DA][Plan<W, CT, NPT>::CTL],
                                           f32x4 (&acc)[Plan<W, CT, NPT>::n]) {
@@ -475,27 +568,34 @@ __device__ __forceinline__ void conv_mfma(const uint8_t *smem, const Geo<Plan<W,
         for (int t = 0; t < NT; ++t)
             if (live(t, kb)) B[kb][t] = *(const uint4 *)(smem + (IN - 256) + (g.b(t, tap) ^ flip));
     }
-#pragma unroll
-    for (int ks = 0; ks < kKStepsRes; ++ks) {
-        constexpr int la = DA - 1, lb = DB - 1;
-#ifdef SPAI_EXP_NO_A
-        if (false) {
-#else
+    constexpr int la = DA - 1, lb = DB - 1;
+    // A for k-step ks + la (this layer's, or the next layer's first k-steps)
+    auto load_a = [&](int ks) {
         if (ks + la < kKStepsRes) {
-#endif
 #pragma unroll
-            for (int c = 0; c < CTL; ++c)
-#ifdef SPAI_EXP_A_FIXED
-                A[(ks + la) % DA][c] = wl[c * 64];
-#else
-                A[(ks + la) % DA][c] = wl[((ks + la) * CT + c) * 64];
-#endif
+            for (int c = 0; c < CTL; ++c) A[(ks + la) % DA][c] = wl[((ks + la) * CT + c) * 64];
         } else {
-#ifndef SPAI_EXP_NO_A
 #pragma unroll
             for (int c = 0; c < CTL; ++c) A[(ks + la) % DA][c] = wnl[((ks + la - kKStepsRes) * CT + c) * 64];
-#endif
         }
+    };
+#pragma unroll
+    for (int ks = 0; ks < kKStepsRes; ++ks) {
+        if constexpr (EPI > 0) if (ks == kKStepsRes - 2) {
+            // B reads of the last k-step (if not issued yet), then the fused final tap;
+            // k-step 17's A prefetch waits for the MFMAs that read the slot it refills
+            if (ks + lb < kKStepsRes) {
+                const int tap = (ks + lb) >> 1, flip = ((ks + lb) & 1) << 6;
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+                    if (live(t, ks + lb)) B[(ks + lb) % DB][t] = *(const uint4 *)(smem + (IN - 256) + (g.b(t, tap) ^ flip));
+            }
+            load_a(ks);
+            final_tap_epilogue<W, CT, NPT, S, DA, DB, EPI, OUT>(smem, g, lane, A, B, bv, acc);
+            load_a(ks + 1);
+            break;
+        }
+        load_a(ks);
         int nr = 0;   // B reads issued this k-step (for the issue-order hints)
         if (ks + lb < kKStepsRes) {
             const int tap = (ks + lb) >> 1, flip = ((ks + lb) & 1) << 6;
@@ -768,14 +868,15 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
     for (int b = 0; b < P.blocks; ++b) {   // relu(x + BN(conv(relu(BN(conv(x)))))), model/mod.rs:152-165
         f32x4 acc[Plan<W, 4, NPT>::n];
         const int l1 = 2 * b, l2 = 2 * b + 1;
-        conv_mfma<W, 4, NPT, S, kX, DA, DB>(smem, g, bias + kHid * (1 + l1), P.w_res + l1 * kLayer, P.w_res + l2 * kLayer, lane, A, acc);
+        conv_mfma<W, 4, NPT, S, kX, DA, DB, SPAI_FUSE_EPI ? 1 : 0, kY>(smem, g, bias + kHid * (1 + l1), P.w_res + l1 * kLayer,
+                                                                    P.w_res + l2 * kLayer, lane, A, acc);
 #ifdef SPAI_DIAG
         if (b == 0 && !kDiagHead) {   // make the k-loop's results visible before the stamp
             asm volatile("" ::"v"(acc[0][0]), "v"(acc[PL4::n - 1][3]));
             stamp(P, W, lane, 17);
         }
 #endif
-        epilogue_act<W, NPT, kY, false>(smem, g, acc);
+        if (!SPAI_FUSE_EPI) epilogue_act<W, NPT, kY, false>(smem, g, acc);
 #ifdef SPAI_DIAG
         if (b == 0 && !kDiagHead) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -787,9 +888,10 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
         if (b == 0 && !kDiagHead) stamp(P, W, lane, 19);
 #endif
         if (l1 < 12) stamp(P, W, lane, 2 + l1);
-        conv_mfma<W, 4, NPT, S, kY, DA, DB>(smem, g, bias + kHid * (1 + l2), P.w_res + l2 * kLayer,
+        conv_mfma<W, 4, NPT, S, kY, DA, DB, SPAI_FUSE_EPI ? 2 : 0, kX>(smem, g, bias + kHid * (1 + l2), P.w_res + l2 * kLayer,
                             b + 1 < P.blocks ? P.w_res + (l2 + 1) * kLayer : P.w_res + l2 * kLayer, lane, A, acc);
-        if (SPAI_RES_MFMA) {
+        if (SPAI_FUSE_EPI) {
+        } else if (SPAI_RES_MFMA) {
             residual_mfma<W, NPT, kX>(smem, g, lane, acc);
             epilogue_act<W, NPT, kX, false>(smem, g, acc);
         } else {
