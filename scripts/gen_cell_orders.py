@@ -8,7 +8,9 @@ kCellOrder[S][r / S] of position r % S.  The search maximises the skipped (tile,
 tap) pairs while keeping the four waves' MFMA counts balanced under the kernel's
 task plans (Plan<W, CT, NPT>: co-major for NPT <= 8, pair split up to 11 tiles,
 position-major above), for the trunk convs (CT = 4) and, at a quarter of the
-weight, the head conv (CT = 3).  At S = 4 the order index's parity must equal
+weight, the head conv as it ran when the tables were searched (its own CT = 3
+plan; since round 3 the head runs on the trunk plan without co tile 3, so the
+trunk term is the one that counts).  At S = 4 the order index's parity must equal
 the cell's checkerboard colour (h + w) & 1: a tile then holds row groups 4t..4t+3
 whose neighbours for any tap alternate in parity, which keeps the B-fragment reads
 bank-conflict free (net_c4.hip make_geo).  S <= 3 keep the position-major rows of

@@ -48,7 +48,6 @@ constexpr int kWaves = 4;
 constexpr int kThreads = kWaves * 64;
 constexpr int kKStepsRes = 18;             // 576 / 32
 constexpr int kHeadC = 35;                 // 32 policy + 3 value channels
-constexpr int kHeadCT = 3;                 // 48 padded co
 constexpr int kPolIn = 32 * c4::kCells;    // 1344
 constexpr int kValIn = 3 * c4::kCells;     // 126
 
@@ -71,14 +70,16 @@ constexpr int kHBytes = kP * 128;          // (all of Y)
 constexpr int kB = kH + kHBytes;           // 8 x (mine, theirs)
 constexpr int kL = kB + kS * 16;           // linear partials [4 waves][8][8] f32
 constexpr int kMaxBlocks = 20;
-constexpr int kBiasFloats = kHid + 2 * kMaxBlocks * kHid + 48;   // stem, residual convs, head
+constexpr int kBiasFloats = kHid + 2 * kMaxBlocks * kHid + kHid;   // stem, residual convs, head (64 padded)
 constexpr int kBias = kL + kWaves * 64 * 4; // all conv biases, staged once per workgroup
 constexpr int kPlanes = kBias + kBiasFloats * 4;   // stem neighbour planes [8][34] u64 (272-B rows: positions
                                                    // in different 16-B bank groups)
 constexpr int kPlaneRow = 34;
 constexpr int kWStem = kPlanes + kS * kPlaneRow * 8;   // stem weight fragments [4 ct][64 lanes] x 16 B, staged once
 constexpr int kTab = kWStem + 4 * 64 * 16;         // k_geo_init: one S's row-group table [42] x 16 B (NetParams::geo)
-constexpr int kLdsBytes = kTab + 42 * 16;
+constexpr int kLinW = kTab + 42 * 16;             // the fused linear's B fragments [48 ks][64 lanes] x 16 B, staged
+                                                   // once per launch by LDS-DMA (stage_linear)
+constexpr int kLdsBytes = kLinW + 48 * 1024;
 constexpr int kStamps = 24;                // phase stamps per wave in the diagnostic mode (17..19: inside block 0 conv1;
                                            // 20/21: s_memtime / s_memrealtime at kernel entry, 22: s_memrealtime at the
                                            // first group's stamp 0, 23: s_memrealtime after the last group)
@@ -88,17 +89,17 @@ static_assert(kLdsBytes <= 160 * 1024, "LDS budget");
 struct NetParams {
     const uint4 *w_stem;   // [4 ct][64 lanes] 16 B fragments
     const uint4 *w_res;    // [2*blocks][18 ks][4 ct][64]
-    const uint4 *w_head;   // [18][3][64]
+    const uint4 *w_head;   // [18][4][64]: a 64-channel layer whose co tile 3 is never computed
     const float *b_stem;   // [64]
     const float *b_res;    // [2*blocks][64]
-    const float *b_head;   // [48]
+    const float *b_head;   // [64]
     const uint4 *w_lin;    // [48 ks][64] B fragments of the fused policy|value linear
     const float *b_pol;    // [7]
     const float *b_val;    // [1]
     // per group size S and row group idx (= LDS row / S): {cell, then the row group
     // holding each 3x3 tap's neighbour cell as 9 bytes (0xFF off the board)} x 16 B
     const uint4 *geo;             // [9][42]
-    const uint4 *lane_geo;        // per-lane geometry of every (S, plan, wave, tile): lane_geo_at, k_geo_init
+    const uint4 *lane_geo;        // per-lane geometry of every (S, wave, tile): lane_geo_at, k_geo_init
     unsigned long long *stamps;   // diagnostic: [grid][4 waves][kStamps] s_memtime, or null
     int blocks;
 };
@@ -339,23 +340,22 @@ __device__ __forceinline__ void make_geo(const uint8_t *smem, int lane, Geo<Plan
 
 // Per-lane geometry table (NetParams::lane_geo), built once per net by
 // k_geo_init from make_geo: computing it in the forward cost ~10 VALU per
-// (tile, tap), some 900 cycles per position tile per plan before the first MFMA.
-// Entry (S, plan, W, t) holds 64 lanes x 32 B: {rel2[5], epi, aux, 0}.  Plan 0 =
-// the 64-channel layers (CT = 4), whose aux feeds the stem: s | (bit col*7+row)
-// << 8 (padding rows: s = S, a zeroed plane row); plan 1 = the head conv (CT = 3),
-// whose aux is the head-feature offset s * lin_pitch(S) + cell * 36, -1 on padding.
+// (tile, tap), some 900 cycles per position tile before the first MFMA.  Entry
+// (S, W, t) of the 64-channel layers' plan (the head conv runs on it too) holds
+// 64 lanes x 32 B: {rel2[5], epi, aux, 0}; aux = s | (bit col*7+row) << 8 for the
+// stem and the head-feature offsets (padding rows: s = S, a zeroed plane row).
 constexpr int kGeoNT = 8;   // the most position tiles a wave holds (S = 3, co-major)
-__host__ __device__ constexpr size_t lane_geo_at(int S, int plan, int W, int t) {
-    return ((((size_t)(S - 1) * 2 + plan) * kWaves + W) * kGeoNT + t) * 64 * 2;   // in uint4
+__host__ __device__ constexpr size_t lane_geo_at(int S, int W, int t) {
+    return (((size_t)(S - 1) * kWaves + W) * kGeoNT + t) * 64 * 2;   // in uint4
 }
-constexpr size_t kLaneGeoU4 = lane_geo_at(kS + 1, 0, 0, 0);
+constexpr size_t kLaneGeoU4 = lane_geo_at(kS + 1, 0, 0);
 
-template <int W, int CT, int NPT, int S>
-__device__ __forceinline__ void load_geo(const NetParams &P, int lane, Geo<Plan<W, CT, NPT>::NT> &g,
-                                         int (&aux)[Plan<W, CT, NPT>::NT]) {
-    constexpr int NT = Plan<W, CT, NPT>::NT;
+template <int W, int NPT, int S>
+__device__ __forceinline__ void load_geo(const NetParams &P, int lane, Geo<Plan<W, 4, NPT>::NT> &g,
+                                         int (&aux)[Plan<W, 4, NPT>::NT]) {
+    constexpr int NT = Plan<W, 4, NPT>::NT;
     static_assert(NT <= kGeoNT, "lane geometry table depth");
-    const uint4 *src = P.lane_geo + lane_geo_at(S, CT == 3, W, 0) + 2 * lane;
+    const uint4 *src = P.lane_geo + lane_geo_at(S, W, 0) + 2 * lane;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
         const uint4 a = src[t * 128], b = src[t * 128 + 1];
@@ -369,57 +369,45 @@ __device__ __forceinline__ void load_geo(const NetParams &P, int lane, Geo<Plan<
     }
 }
 
-template <int S, int CT, int W>
+template <int S, int W>
 __device__ void geo_init_one(const uint8_t *smem, uint4 *out, int lane) {
     constexpr int NPT = npt_of(S);
-    using PL = Plan<W, CT, NPT>;
+    using PL = Plan<W, 4, NPT>;
     Geo<PL::NT> g;
-    make_geo<W, CT, NPT, S>(smem, lane, g);
-    uint4 *dst = out + lane_geo_at(S, CT == 3, W, 0) + 2 * lane;
+    make_geo<W, 4, NPT, S>(smem, lane, g);
+    uint4 *dst = out + lane_geo_at(S, W, 0) + 2 * lane;
     for (int t = 0; t < PL::NT; ++t) {
         const RowCell rc = row_cell<S>(smem, PL::gpt(t) * 16 + (lane & 15));
-        int aux;
-        if (CT == 4) {
-            const int h = rc.cell / c4::kCols, w = rc.cell - h * c4::kCols;
-            aux = rc.cell < 0 ? S : rc.s | (w * 7 + h) << 8;
-        } else {
-            aux = rc.cell < 0 ? -1 : rc.s * lin_pitch(S) + rc.cell * kHC;
-        }
+        const int h = rc.cell / c4::kCols, w = rc.cell - h * c4::kCols;
+        const int aux = rc.cell < 0 ? S : rc.s | (w * 7 + h) << 8;
         dst[t * 128] = make_uint4(g.rel2[t][0], g.rel2[t][1], g.rel2[t][2], g.rel2[t][3]);
         dst[t * 128 + 1] = make_uint4(g.rel2[t][4], (uint32_t)g.epi[t], (uint32_t)aux, 0u);
     }
 }
 
 template <int S>
-__device__ void geo_init_s(const uint8_t *smem, uint4 *out, int plan, int W, int lane) {
-    if (plan == 0) {
-        if (W == 0) geo_init_one<S, 4, 0>(smem, out, lane);
-        else if (W == 1) geo_init_one<S, 4, 1>(smem, out, lane);
-        else if (W == 2) geo_init_one<S, 4, 2>(smem, out, lane);
-        else geo_init_one<S, 4, 3>(smem, out, lane);
-    } else {
-        if (W == 0) geo_init_one<S, 3, 0>(smem, out, lane);
-        else if (W == 1) geo_init_one<S, 3, 1>(smem, out, lane);
-        else if (W == 2) geo_init_one<S, 3, 2>(smem, out, lane);
-        else geo_init_one<S, 3, 3>(smem, out, lane);
-    }
+__device__ void geo_init_s(const uint8_t *smem, uint4 *out, int W, int lane) {
+    if (W == 0) geo_init_one<S, 0>(smem, out, lane);
+    else if (W == 1) geo_init_one<S, 1>(smem, out, lane);
+    else if (W == 2) geo_init_one<S, 2>(smem, out, lane);
+    else geo_init_one<S, 3>(smem, out, lane);
 }
 
-// one 64-thread workgroup per (S, plan, wave): blockIdx.x = ((S - 1) * 2 + plan) * 4 + W
+// one 64-thread workgroup per (S, wave): blockIdx.x = (S - 1) * 4 + W
 __global__ __launch_bounds__(64) void k_geo_init(const uint4 *__restrict__ geo, uint4 *__restrict__ out) {
     __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
-    const int S = blockIdx.x / 8 + 1, plan = (blockIdx.x / 4) & 1, W = blockIdx.x & 3, lane = threadIdx.x;
+    const int S = blockIdx.x / kWaves + 1, W = blockIdx.x % kWaves, lane = threadIdx.x;
     if (lane < c4::kCells) ((uint4 *)(smem + kTab))[lane] = geo[S * c4::kCells + lane];
     __syncthreads();
     switch (S) {
-    case 1: geo_init_s<1>(smem, out, plan, W, lane); break;
-    case 2: geo_init_s<2>(smem, out, plan, W, lane); break;
-    case 3: geo_init_s<3>(smem, out, plan, W, lane); break;
-    case 4: geo_init_s<4>(smem, out, plan, W, lane); break;
-    case 5: geo_init_s<5>(smem, out, plan, W, lane); break;
-    case 6: geo_init_s<6>(smem, out, plan, W, lane); break;
-    case 7: geo_init_s<7>(smem, out, plan, W, lane); break;
-    default: geo_init_s<8>(smem, out, plan, W, lane); break;
+    case 1: geo_init_s<1>(smem, out, W, lane); break;
+    case 2: geo_init_s<2>(smem, out, W, lane); break;
+    case 3: geo_init_s<3>(smem, out, W, lane); break;
+    case 4: geo_init_s<4>(smem, out, W, lane); break;
+    case 5: geo_init_s<5>(smem, out, W, lane); break;
+    case 6: geo_init_s<6>(smem, out, W, lane); break;
+    case 7: geo_init_s<7>(smem, out, W, lane); break;
+    default: geo_init_s<8>(smem, out, W, lane); break;
     }
 }
 
@@ -456,11 +444,13 @@ __device__ __forceinline__ void final_tap_epilogue(uint8_t *smem, const Geo<Plan
                                                    const uint4 (&A)[DA][Plan<W, CT, NPT>::CTL],
                                                    const uint4 (&B)[DB][Plan<W, CT, NPT>::NT],
                                                    const f32x4 (&bv)[Plan<W, CT, NPT>::CTL],
-                                                   f32x4 (&acc)[Plan<W, CT, NPT>::n]) {
+                                                   f32x4 (&acc)[Plan<W, CT, NPT>::n],
+                                                   const int (&hoff)[Plan<W, CT, NPT>::NT]) {
     using PL = Plan<W, CT, NPT>;
     constexpr int n = PL::n, k0 = kKStepsRes - 2, D = 2;
     static_assert(CT == 4, "fused epilogue: 64-channel layers");
     auto live = [](int t, int ks) { return !((tap_skip(S, PL::gpt(t)) >> (ks >> 1)) & 1); };
+    auto task_on = [](int i) { return !(EPI == 3 && PL::co(i) == 3); };   // the head has no co tile 3
     uint4 id[2];   // residual identities (residual_mfma)
     uint4 rb[3];   // residual B fragments, two tasks ahead
     if (EPI == 2) {
@@ -488,7 +478,7 @@ __device__ __forceinline__ void final_tap_epilogue(uint8_t *smem, const Geo<Plan
             const int t = PL::gpt(PL::pt(i)), c = PL::co(i) - PL::C0;
 #pragma unroll
             for (int ks = k0; ks < kKStepsRes; ++ks)
-                if (live(PL::pt(i), ks)) {
+                if (task_on(i) && live(PL::pt(i), ks)) {
                     acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[ks % DA][c]), as_bf16x8(B[ks % DB][PL::pt(i)]),
                                                                     ks == first_kstep(S, t) ? bv[c] : acc[i], 0, 0, 0);
                     ++nm;
@@ -499,10 +489,17 @@ __device__ __forceinline__ void final_tap_epilogue(uint8_t *smem, const Geo<Plan
                 ++nm;
             }
         }
-        if (i >= D) {
+        if (i >= D && EPI < 3) {
             const int j = i - D;
             const int off = OUT + (g.epi[PL::pt(j)] ^ (PL::co(j) << 5));
             *(uint2 *)(smem + off) = make_uint2(pack_relu_bf16x2(acc[j][0], acc[j][1]), pack_relu_bf16x2(acc[j][2], acc[j][3]));
+            nv = 5;
+            nw = 1;
+        } else if (i >= D && task_on(i - D)) {   // the head: H[s][cell * 36 + c] for the 35 real channels
+            const int j = i - D, co0 = PL::co(j) * 16 + 4 * (lane >> 4), off = hoff[PL::pt(j)];
+            // a lane with nothing to store writes its own word of the (not yet used) linear partials
+            const int addr = co0 < kHC && off >= 0 ? kH + 2 * (off + co0) : kL + 8 * lane;
+            *(uint2 *)(smem + addr) = make_uint2(pack_relu_bf16x2(acc[j][0], acc[j][1]), pack_relu_bf16x2(acc[j][2], acc[j][3]));
             nv = 5;
             nw = 1;
         }
@@ -544,7 +541,8 @@ template <int W, int CT, int NPT, int S, int IN, int DA, int DB, int EPI = 0, in
 __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, NPT>::NT> &g, const float *bias,
                                           const uint4 *__restrict__ w, const uint4 *__restrict__ wn, int lane,
                                           uint4 (&A)[DA][Plan<W, CT, NPT>::CTL],
-                                          f32x4 (&acc)[Plan<W, CT, NPT>::n]) {
+                                          f32x4 (&acc)[Plan<W, CT, NPT>::n],
+                                          const int (&hoff)[Plan<W, CT, NPT>::NT]) {
     using PL = Plan<W, CT, NPT>;
     constexpr int NT = PL::NT, CTL = PL::CTL;
     static_assert(kKStepsRes % DA == 0, "the carried A ring needs DA | k-steps per layer");
@@ -559,7 +557,15 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
     const uint4 *wnl = wn + PL::C0 * 64 + lane;
     // (tile, tap) pairs whose rows are all off the board for that tap are skipped
     // (tap_skip); the indices below are compile-time constants once unrolled
-    auto live = [](int t, int ks) { return !((tap_skip(S, PL::gpt(t)) >> (ks >> 1)) & 1); };
+    // EPI = 3, the head conv: co tile 3 (channels 48..63) does not exist -- its
+    // tasks, weight loads, and the B reads of tiles with no other task are dropped
+    auto task_on = [](int i) { return !(EPI == 3 && PL::co(i) == 3); };
+    auto tile_on = [&](int t) {
+        bool on = false;
+        for (int i = 0; i < PL::n; ++i) on = on || (PL::pt(i) == t && task_on(i));
+        return on;
+    };
+    auto live = [&](int t, int ks) { return tile_on(t) && !((tap_skip(S, PL::gpt(t)) >> (ks >> 1)) & 1); };
     uint4 B[DB][NT];
 #pragma unroll
     for (int kb = 0; kb < DB - 1; ++kb) {
@@ -573,8 +579,9 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
     auto load_a = [&](int ks) {
         if (ks + la < kKStepsRes) {
 #pragma unroll
-            for (int c = 0; c < CTL; ++c) A[(ks + la) % DA][c] = wl[((ks + la) * CT + c) * 64];
-        } else {
+            for (int c = 0; c < CTL; ++c)
+                if (!(EPI == 3 && PL::C0 + c == 3)) A[(ks + la) % DA][c] = wl[((ks + la) * CT + c) * 64];
+        } else if (EPI != 3) {   // (nothing follows the head)
 #pragma unroll
             for (int c = 0; c < CTL; ++c) A[(ks + la) % DA][c] = wnl[((ks + la - kKStepsRes) * CT + c) * 64];
         }
@@ -591,7 +598,7 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
                     if (live(t, ks + lb)) B[(ks + lb) % DB][t] = *(const uint4 *)(smem + (IN - 256) + (g.b(t, tap) ^ flip));
             }
             load_a(ks);
-            final_tap_epilogue<W, CT, NPT, S, DA, DB, EPI, OUT>(smem, g, lane, A, B, bv, acc);
+            final_tap_epilogue<W, CT, NPT, S, DA, DB, EPI, OUT>(smem, g, lane, A, B, bv, acc, hoff);
             load_a(ks + 1);
             break;
         }
@@ -609,7 +616,7 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
         int nm = 0;
 #pragma unroll
         for (int i = 0; i < PL::n; ++i)
-            if (live(PL::pt(i), ks)) {
+            if (task_on(i) && live(PL::pt(i), ks)) {
                 const int t = PL::gpt(PL::pt(i));
                 acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[ks % DA][PL::co(i) - PL::C0]),
                                                                 as_bf16x8(B[ks % DB][PL::pt(i)]),
@@ -767,51 +774,50 @@ __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const fl
     epilogue_act<W, NPT, kX, false>(smem, g, acc);
 }
 
-constexpr int kLinPerWave = 12;
+// The fused linear's weights into LDS (kLinW): wave W copies k-steps
+// [12W, 12W+12) with global_load_lds (1 KiB per instruction, no VGPRs).  Issued
+// at the head conv's start: while such a copy is in flight the compiler waits
+// for every outstanding vector load at the next use of a register load, and the
+// head's first register-loaded weights are used DA-1 k-steps later (its first
+// fragments were prefetched by the last residual conv), by which time the copy
+// has landed.  torso_and_heads waits for it (vmcnt(0) + the head's barrier)
+// before the linear reads it.
 template <int W>
-__device__ __forceinline__ void load_lin(const NetParams &P, int lane, uint4 (&wl)[kLinPerWave]) {
-    constexpr int k0 = kLinPerWave * W;
+__device__ __forceinline__ void stage_linear(uint8_t *smem, const NetParams &P, int lane) {
 #pragma unroll
-    for (int i = 0; i < kLinPerWave; ++i)
-        if (k0 + i < kLinKSteps) wl[i] = P.w_lin[(k0 + i) * 64 + lane];
+    for (int i = 0; i < kLinKSteps / kWaves; ++i) {
+        const int ks = W * (kLinKSteps / kWaves) + i;
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)(P.w_lin + ks * 64 + lane),
+                                         (void __attribute__((address_space(3))) *)(smem + kLinW + ks * 1024), 16, 0, 0);
+    }
 }
 
-#ifndef SPAI_LIN_LATE
-#define SPAI_LIN_LATE 0
-#endif
-template <int W, int S>
-__device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, int lane, uint4 (&wl)[kLinPerWave]) {
+// The head conv (64 -> 32 policy + 3 value channels) on the 64-channel layers'
+// plan, geometry and A ring: the last residual conv prefetches its first
+// weights, and co tile 3 is dropped (conv_mfma EPI = 3), whose fused epilogue
+// writes relu(bf16) features to H[s][cell * 36 + c].
+template <int W, int S, int DA>
+__device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, int lane,
+                                           const Geo<Plan<W, 4, npt_of(S)>::NT> &g,
+                                           const int (&aux)[Plan<W, 4, npt_of(S)>::NT],
+                                           uint4 (&A)[DA][Plan<W, 4, npt_of(S)>::CTL]) {
     constexpr int NPT = npt_of(S);
-    using PL = Plan<W, kHeadCT, NPT>;
-    Geo<PL::NT> g;
+    using PL = Plan<W, 4, NPT>;
     int hoff[PL::NT];   // head-feature offset of each tile's row (-1: padding)
-    load_geo<W, kHeadCT, NPT, S>(P, lane, g, hoff);
-    f32x4 acc[PL::n];
-    constexpr int DA = a_depth(S), DB = b_depth(S);
-    uint4 A[DA][PL::CTL];
-    load_a_first<kHeadCT, PL::C0, PL::CTL, DA>(P.w_head, lane, A);
-    // the linear's weights after the conv's first fragments: the loads return in order
-    if (!SPAI_LIN_LATE) load_lin<W>(P, lane, wl);
-    conv_mfma<W, kHeadCT, NPT, S, kX, DA, DB>(smem, g, (const float *)(smem + kBias) + kHid * (1 + 2 * P.blocks), P.w_head, P.w_head,
-                              lane, A, acc);
-#ifdef SPAI_DIAG
-    if (kDiagHead) {
-        asm volatile("" ::"v"(acc[0][0]), "v"(acc[PL::n - 1][3]));
-        stamp(P, W, lane, 17);
-    }
-#endif
-    if (SPAI_LIN_LATE) load_lin<W>(P, lane, wl);
-    const int q = lane >> 4;
-    uint16_t *H = (uint16_t *)(smem + kH);
 #pragma unroll
-    for (int i = 0; i < PL::n; ++i) {
-        const int co0 = PL::co(i) * 16 + 4 * q;   // pad channels (zero weights and bias) come out as 0
-        const int off = hoff[PL::pt(i)];
-        if (co0 < kHC && off >= 0)   // H[s][cell * 36 + c] whatever the row order: the linear sums the same K order
-            *(uint2 *)(H + off + co0) =
-                make_uint2(pack_relu_bf16x2(acc[i][0], acc[i][1]), pack_relu_bf16x2(acc[i][2], acc[i][3]));
+    for (int t = 0; t < PL::NT; ++t) {
+        const int s = aux[t] & 255, b = aux[t] >> 8;   // b = col*7 + row
+        hoff[t] = s < S ? s * lin_pitch(S) + ((b % c4::kCols) * c4::kCols + b / c4::kCols) * kHC : -1;
     }
+    stage_linear<W>(smem, P, lane);
+    f32x4 acc[PL::n];
+    conv_mfma<W, 4, NPT, S, kX, DA, b_depth(S), 3, kH>(smem, g, (const float *)(smem + kBias) + kHid * (1 + 2 * P.blocks),
+                                                      P.w_head, P.w_head, lane, A, acc, hoff);
+#ifdef SPAI_DIAG
+    if (kDiagHead) stamp(P, W, lane, 17);
+#endif
     // K padding [1512, 1536) of each row: 6 words of 8 B
+    uint16_t *H = (uint16_t *)(smem + kH);
     if (W == 0 && lane < S * 6)
         *(uint2 *)(H + (lane / 6) * lin_pitch(S) + kLinFeat + 4 * (lane % 6)) = make_uint2(0u, 0u);
 #ifdef SPAI_DIAG
@@ -825,12 +831,10 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
 // fused policy|value linear on MFMA: out[s][o] = sum_k H[s][k] * Wl[o][k]
 // (o < 7 policy logits over k < 1344, o = 7 value pre-activation over
 // 1344 <= k < 1470; connect_four.rs:63-64,69-70).  Wave W takes k-steps
-// [12W, 12W+12) of 48 (weights loaded by load_lin behind the head conv's first fragments);
-// partial sums go to LDS.
+// [12W, 12W+12) of 48 (B fragments from LDS, stage_linear); partial sums go to LDS.
 template <int W, int S>
-__device__ __forceinline__ void linear_mfma(uint8_t *smem, const uint4 (&wl)[kLinPerWave], int lane) {
-    constexpr int k0 = kLinPerWave * W;
-    constexpr int k1 = (kLinPerWave * (W + 1) < kLinKSteps) ? kLinPerWave * (W + 1) : kLinKSteps;
+__device__ __forceinline__ void linear_mfma(uint8_t *smem, int lane) {
+    constexpr int k0 = (kLinKSteps / kWaves) * W, k1 = k0 + kLinKSteps / kWaves;
     const int s = lane & 15, q = lane >> 4;
     const uint8_t *hrow = s < S ? smem + kH + s * lin_pitch(S) * 2 + q * 16 : smem + kZ + q * 16;
     const int hstep = s < S ? 64 : 0;
@@ -838,7 +842,7 @@ __device__ __forceinline__ void linear_mfma(uint8_t *smem, const uint4 (&wl)[kLi
 #pragma unroll
     for (int ks = k0; ks < k1; ++ks) {
         const uint4 a = *(const uint4 *)(hrow + ks * hstep);
-        const uint4 b = wl[ks - k0];
+        const uint4 b = *(const uint4 *)(smem + kLinW + ks * 1024 + lane * 16);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(b), acc, 0, 0, 0);
     }
     float *L = (float *)(smem + kL) + W * 64;   // D[row s = 4q + r][col o = lane & 15]
@@ -858,7 +862,7 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
     const float *bias = (const float *)(smem + kBias);
     constexpr int DA = a_depth(S), DB = b_depth(S);
     uint4 A[DA][PL4::CTL];
-    if (P.blocks > 0) load_a_first<4, PL4::C0, PL4::CTL, DA>(P.w_res, lane, A);
+    load_a_first<4, PL4::C0, PL4::CTL, DA>(P.blocks > 0 ? P.w_res : P.w_head, lane, A);
     stem<W, S, FROM_X>(smem, P, x, base, valid, lane, g, aux);
     __syncthreads();
     stamp(P, W, lane, 1);
@@ -869,7 +873,7 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
         f32x4 acc[Plan<W, 4, NPT>::n];
         const int l1 = 2 * b, l2 = 2 * b + 1;
         conv_mfma<W, 4, NPT, S, kX, DA, DB, SPAI_FUSE_EPI ? 1 : 0, kY>(smem, g, bias + kHid * (1 + l1), P.w_res + l1 * kLayer,
-                                                                    P.w_res + l2 * kLayer, lane, A, acc);
+                                                                    P.w_res + l2 * kLayer, lane, A, acc, aux);
 #ifdef SPAI_DIAG
         if (b == 0 && !kDiagHead) {   // make the k-loop's results visible before the stamp
             asm volatile("" ::"v"(acc[0][0]), "v"(acc[PL4::n - 1][3]));
@@ -889,7 +893,7 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
 #endif
         if (l1 < 12) stamp(P, W, lane, 2 + l1);
         conv_mfma<W, 4, NPT, S, kY, DA, DB, SPAI_FUSE_EPI ? 2 : 0, kX>(smem, g, bias + kHid * (1 + l2), P.w_res + l2 * kLayer,
-                            b + 1 < P.blocks ? P.w_res + (l2 + 1) * kLayer : P.w_res + l2 * kLayer, lane, A, acc);
+                            b + 1 < P.blocks ? P.w_res + (l2 + 1) * kLayer : P.w_head, lane, A, acc, aux);
         if (SPAI_FUSE_EPI) {
         } else if (SPAI_RES_MFMA) {
             residual_mfma<W, NPT, kX>(smem, g, lane, acc);
@@ -900,12 +904,12 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
         __syncthreads();
         if (l2 < 12) stamp(P, W, lane, 2 + l2);
     }
-    uint4 wl[kLinPerWave];
     if (kDiagHead) stamp(P, W, lane, 19);   // diagnostic head mode: 19 = before the head, 17 = head k-loop, 18 = H written
-    head_layer<W, S>(smem, P, lane, wl);
+    head_layer<W, S, DA>(smem, P, lane, g, aux, A);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stage_linear copies have landed
     __syncthreads();
     stamp(P, W, lane, 14);
-    linear_mfma<W, S>(smem, wl, lane);
+    linear_mfma<W, S>(smem, lane);
 }
 
 // Group size for `count` leaves on `grid` workgroups: the fewest rounds R of at
@@ -935,7 +939,7 @@ __device__ __forceinline__ void run_groups(uint8_t *smem, const NetParams &P, ui
     {
         float *bias = (float *)(smem + kBias);
         const int nres = 2 * P.blocks * kHid;
-        for (int i = tid; i < kHid + nres + 48; i += kThreads)
+        for (int i = tid; i < kHid + nres + kHid; i += kThreads)
             bias[i] = i < kHid ? P.b_stem[i] : i < kHid + nres ? P.b_res[i - kHid] : P.b_head[i - kHid - nres];
     }
     for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
@@ -948,7 +952,7 @@ __device__ __forceinline__ void run_groups(uint8_t *smem, const NetParams &P, ui
         ln &= 63;   // restore the known range for the compiler
         Geo<Plan<W, 4, npt_of(S)>::NT> g;
         int aux[Plan<W, 4, npt_of(S)>::NT];
-        load_geo<W, 4, npt_of(S), S>(P, ln, g, aux);   // before the bitboard loads: the two latencies overlap
+        load_geo<W, npt_of(S), S>(P, ln, g, aux);   // before the bitboard loads: the two latencies overlap
         const int base = grp * S;
         const int valid = min(S, (int)count - base);
         if (tid < kS) {
@@ -1188,10 +1192,10 @@ int net_create(spai_engine *e, int blocks, int hidden, const float *params, size
     std::vector<float> pw, pb, vw, vb;
     fold(pol_c, pw, pb);
     fold(val_c, vw, vb);
-    std::vector<uint16_t> wh((size_t)kKStepsRes * kHeadCT * 64 * 8, 0);
-    std::vector<float> bh(48, 0.f);
+    std::vector<uint16_t> wh((size_t)kKStepsRes * 4 * 64 * 8, 0);
+    std::vector<float> bh(kHid, 0.f);
     for (int ks = 0; ks < kKStepsRes; ++ks)
-        for (int ct = 0; ct < kHeadCT; ++ct)
+        for (int ct = 0; ct < 4; ++ct)
             for (int l = 0; l < 64; ++l)
                 for (int j = 0; j < 8; ++j) {
                     int co = ct * 16 + (l & 15), k = ks * 32 + 8 * (l >> 4) + j;
@@ -1199,7 +1203,7 @@ int net_create(spai_engine *e, int blocks, int hidden, const float *params, size
                     float v = 0.f;
                     if (co < 32) v = pw[((size_t)co * kHid + ci) * 9 + tap];
                     else if (co < kHeadC) v = vw[((size_t)(co - 32) * kHid + ci) * 9 + tap];
-                    wh[(((size_t)ks * kHeadCT + ct) * 64 + l) * 8 + j] = f2bf(v);
+                    wh[(((size_t)ks * 4 + ct) * 64 + l) * 8 + j] = f2bf(v);
                 }
     for (int o = 0; o < 32; ++o) bh[o] = pb[o];
     for (int o = 0; o < 3; ++o) bh[32 + o] = vb[o];
@@ -1263,7 +1267,7 @@ int net_create(spai_engine *e, int blocks, int hidden, const float *params, size
     up(n->geo, geo);
     if (rc == SPAI_OK) rc = n->lane_geo.alloc(kLaneGeoU4 * 4);
     if (rc == SPAI_OK) {
-        k_geo_init<<<kS * 2 * kWaves, 64, 0, e->stream>>>((const uint4 *)n->geo.p, (uint4 *)n->lane_geo.p);
+        k_geo_init<<<kS * kWaves, 64, 0, e->stream>>>((const uint4 *)n->geo.p, (uint4 *)n->lane_geo.p);
         if (hipGetLastError() != hipSuccess || hipStreamSynchronize(e->stream) != hipSuccess) {
             set_error("lane geometry kernel failed");
             rc = SPAI_ERR_DEVICE;
