@@ -70,7 +70,7 @@ def parse():
     ap.add_argument("--rules-bench", action="store_true", help="also time the batched rules kernels")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events (A/B of their cost)")
     ap.add_argument("--no-isolated", action="store_true", help="skip the isolated-forward measurement")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r02", "final", "forward_traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r03", "final", "forward_traffic.json"),
                     help="PMC summary (scripts/gpu_traffic.sh) of this bench command: HBM bytes per k_forward launch")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
@@ -258,14 +258,16 @@ def main():
     if dist.rank == 0 and not args.no_isolated:
         iso = {}
         mean_leaves = int(round(ev["items"] / max(1, ev["launches"])))
+        net.bench(G, iters=1500)   # ~0.2 s of launches first: time at the clock the GPU holds under load
         for n in sorted({max(1, mean_leaves), max(1, 2 * mean_leaves), G // 2, G}):
-            ms = net.bench(n, iters=40)
+            ms = net.bench(n, iters=300)
             tf = fpe * n / (ms * 1e-3) / 1e12
             iso[str(n)] = {"ms": ms, "TFLOP/s": tf, "frac": tf / BF16_PEAK_TFLOPS}
         result["roofline"]["isolated"] = iso
         result["roofline"]["isolated_note"] = ("k_forward alone on the GPU at N leaves per launch (spai_net_bench: "
-                                               "40 back-to-back launches between HIP events); the timed region's "
-                                               "per-launch figure shares the CUs with the other search chain")
+                                               "300 back-to-back launches between HIP events, after ~0.2 s of "
+                                               "warm-up launches); the timed region's per-launch figure shares the "
+                                               "CUs with the other search chain")
     if args.rules_bench and dist.rank == 0:
         n = 1 << 24
         ms = eng.rules_bench(n, iters=10)
