@@ -655,9 +655,7 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
         double ev = 0;
         const auto tm0 = std::chrono::steady_clock::now();
         SPAI_TRY(search(e, na, active.data(), e->cfg.num_searches, pol.data(), ids.data(), vis.data(), nch.data(), &ev));
-        if (trace)
-            std::fprintf(trace, "%llu,%u,%.0f,%.6f\n", (unsigned long long)move_no, na, ev,
-                         std::chrono::duration<double>(std::chrono::steady_clock::now() - tm0).count());
+        const auto tm1 = std::chrono::steady_clock::now();
         sims += (double)na * e->cfg.num_searches;
         evals += ev;
         moves += 1;
@@ -708,6 +706,10 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
             }
         }
         SPAI_TRY(upload_roots(e, 0, T.n_trees));
+        if (trace)   // move, active trees, leaves evaluated, search seconds, host seconds (sampling + root upload)
+            std::fprintf(trace, "%llu,%u,%.0f,%.6f,%.6f\n", (unsigned long long)move_no, na, ev,
+                         std::chrono::duration<double>(tm1 - tm0).count(),
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - tm1).count());
         ++move_no;
     }
     if (trace) std::fclose(trace);
