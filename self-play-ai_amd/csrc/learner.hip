@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "spai_internal.h"
@@ -139,7 +140,7 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
     extern __shared__ float sm[];
     float *xs = sm;                          // [CINP][kPlane]
     float *red = sm + CINP * kPlane;         // K-split partials [3 parts][3 mt][64 lanes][4] per channel tile
-    const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int b = blockIdx.x, lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int nt = wave % NT, part = wave / NT;
     const int s0 = part * PER;
     const int row = lane & 15, kq = lane >> 4;
@@ -154,27 +155,43 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
     // MTS = 3: the workgroup covers all 3 position tiles and blockIdx.y picks the
     // channel slice; MTS = 1: blockIdx.y picks the position tile (all channels)
     const int mt0 = MTS == 3 ? 0 : (int)blockIdx.y;
-    int pbase[MTS];
-    bool pval[MTS];
+    // per-lane A base of each position tile, biased by the most negative tap
+    // offset (-10) so every k-step's offset is a non-negative immediate.  Rows past
+    // the 42 cells read cell 0: D row i depends only on A row i, and those rows are
+    // never stored, so the k-loop has no select (a per-MFMA exec branch kept the
+    // scheduler from running LDS reads ahead: one exposed LDS round trip per MFMA)
+    const float *xb[MTS];
 #pragma unroll
     for (int mt = 0; mt < MTS; ++mt) {
         const int p = (mt0 + mt) * 16 + row;
-        pval[mt] = p < kCells;
-        const int pp = pval[mt] ? p : 0;
-        pbase[mt] = (pp / kCols + 1) * 9 + pp % kCols + 1;
+        const int pp = p < kCells ? p : 0;
+        xb[mt] = xs + kq * kPlane + (pp / kCols + 1) * 9 + pp % kCols + 1 - 10;
     }
     f32x4 acc[MTS];
 #pragma unroll
     for (int mt = 0; mt < MTS; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // the wave's K part as a compile-time constant: every LDS offset is an immediate
+    auto kloop = [&](auto part_c) {
+        constexpr int s0c = decltype(part_c)::value * PER;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-        const int s = s0 + i, tap = s / CSN, cs = s % CSN;   // CSN is a power of two here: shifts
-        const float *xc = xs + (4 * cs + kq) * kPlane + tap_off(tap);
+        for (int i = 0; i < PER; ++i) {
+            const int s = s0c + i, tap = s / CSN, cs = s % CSN;
+            const int off = 4 * cs * kPlane + tap_off(tap) + 10;
 #pragma unroll
-        for (int mt = 0; mt < MTS; ++mt) {
-            const float av = pval[mt] ? xc[pbase[mt]] : 0.f;
-            acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bq[i], acc[mt], 0, 0, 0);
+            for (int mt = 0; mt < MTS; ++mt)
+                acc[mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[mt][off], bq[i], acc[mt], 0, 0, 0);
         }
+    };
+    if constexpr (KS == 1) {
+        kloop(std::integral_constant<int, 0>{});
+    } else if constexpr (KS == 2) {
+        if (part == 0) kloop(std::integral_constant<int, 0>{});
+        else kloop(std::integral_constant<int, 1>{});
+    } else {
+        if (part == 0) kloop(std::integral_constant<int, 0>{});
+        else if (part == 1) kloop(std::integral_constant<int, 1>{});
+        else if (part == 2) kloop(std::integral_constant<int, 2>{});
+        else kloop(std::integral_constant<int, 3>{});
     }
     if (KS > 1) {   // fixed-order sum of the K parts
         if (part > 0) {
@@ -238,32 +255,57 @@ __global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict
     const int row = lane & 15, kq = lane >> 4;
     // this wave's tiles: group's range [t0, t1), wave-strided
     const int t0 = ntiles * group / groups, t1 = ntiles * (group + 1) / groups;
+    // positions past the 42 cells read cell 0's plane entry: their dz (A) is zero
+    // in ds, so the products are exact zeros, and the k-loop needs no select
     int pb[11];
-    bool pv[11];
 #pragma unroll
     for (int s = 0; s < 11; ++s) {
         const int p = 4 * s + kq;
-        pv[s] = p < kCells;
-        const int pp = pv[s] ? p : 0;
+        const int pp = p < kCells ? p : 0;
         pb[s] = (pp / kCols + 1) * 9 + pp % kCols + 1;
     }
     f32x4 acc[kWgMaxTiles];
 #pragma unroll
     for (int j = 0; j < kWgMaxTiles; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int b0 = chunk * kWgSamples, b1 = min(B, b0 + kWgSamples);
-    // the next sample's planes and dz rows are loaded into registers while the
-    // current sample's MFMAs run (one exposed round trip per chunk, not per sample)
-    float vx[kStageMax], vd[kDzMax];
-    load_planes(x + (size_t)b0 * cin * kCells, cin, CINP, vx);
-    load_dz(dz + (size_t)b0 * cout * kCells, cout, coutp, vd);
+    // Staging: the zero borders of the planes, the padding channels and the dz
+    // padding (positions 42, 43, rows >= cout) are written once; each sample then
+    // copies only its cin x 42 inputs and cout x 42 dz values, both contiguous in
+    // memory (coalesced loads at immediate offsets), to LDS destinations computed
+    // once per workgroup.  The next sample's values are loaded into registers
+    // while the current sample's MFMAs run.
+    constexpr int NX = (CINP * kCells + kThreads - 1) / kThreads;   // 11 at 64 channels
+    constexpr int ND = (64 * kCells + kThreads - 1) / kThreads;     // cout <= 64
+    const int nx = cin * kCells, nd = cout * kCells;
+    for (int i = threadIdx.x; i < CINP * kPlane + coutp * 44; i += kThreads) sm[i] = 0.f;
+    int dx[NX], dd[ND];
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+        const int i = threadIdx.x + j * kThreads, c = i / kCells, cell = i - c * kCells;
+        dx[j] = i < nx ? c * kPlane + (cell / kCols + 1) * 9 + cell % kCols + 1 : 0;   // 0: a border cell (gets 0)
+    }
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+        const int i = threadIdx.x + j * kThreads, n = i / kCells, p = i - n * kCells;
+        dd[j] = i < nd ? CINP * kPlane + n * 44 + p : CINP * kPlane + kCells;   // a zero pad (gets 0)
+    }
+    float vx[NX], vd[ND];
+    auto load = [&](int b) {
+        const float *xb = x + (size_t)b * nx, *db = dz + (size_t)b * nd;
+#pragma unroll
+        for (int j = 0; j < NX; ++j) vx[j] = threadIdx.x + j * kThreads < nx ? xb[threadIdx.x + j * kThreads] : 0.f;
+#pragma unroll
+        for (int j = 0; j < ND; ++j) vd[j] = threadIdx.x + j * kThreads < nd ? db[threadIdx.x + j * kThreads] : 0.f;
+    };
+    load(b0);
+    __syncthreads();   // the zero fill lands before any sample's values
     for (int b = b0; b < b1; ++b) {
-        store_planes(vx, CINP, xs);
-        store_dz(vd, coutp, ds);
+#pragma unroll
+        for (int j = 0; j < NX; ++j) sm[dx[j]] = vx[j];   // past the inputs: a 0 into a zero cell
+#pragma unroll
+        for (int j = 0; j < ND; ++j) sm[dd[j]] = vd[j];
         __syncthreads();
-        if (b + 1 < b1) {
-            load_planes(x + (size_t)(b + 1) * cin * kCells, cin, CINP, vx);
-            load_dz(dz + (size_t)(b + 1) * cout * kCells, cout, coutp, vd);
-        }
+        if (b + 1 < b1) load(b + 1);
 #pragma unroll
         for (int j = 0; j < kWgMaxTiles; ++j) {
             const int t = t0 + wave + 4 * j;
@@ -273,11 +315,12 @@ __global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict
             const int k = kt * 16 + row;                      // B[kk = position][n = k]
             const bool kval = k < K;
             const int tap = k / CINP, c = k % CINP;           // CINP: compile-time
-            const int col = kval ? c * kPlane + tap_off(tap) : 0;
+            // a padding column (k >= K) reads position data too: its D column is never stored
+            const float *xcol = xs + (kval ? c * kPlane + tap_off(tap) : 0);
 #pragma unroll
             for (int s = 0; s < 11; ++s) {
                 const float av = arow[4 * s + kq];
-                const float bv = (kval && pv[s]) ? xs[col + pb[s]] : 0.f;
+                const float bv = xcol[pb[s]];
                 acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[j], 0, 0, 0);
             }
         }

@@ -65,13 +65,23 @@ constexpr int kLinFeat = kHC * 42;         // 1512
 constexpr int kLinK = 1536;                // padded to 48 k-steps of 32
 constexpr int kLinKSteps = kLinK / 32;     // 48
 constexpr int kLinPitch = kLinK + 16;      // the largest head-feature pitch (lin_pitch) sizes the overlay
+// The fused linear has 8 outputs (7 logits + the value), so an MFMA B fragment
+// of 16 columns would be half zeros.  SPAI_LIN_HALVES packs the two K halves
+// into the 16 columns instead: column n = (output n & 7, K half n >> 3), A row
+// m = (position m & 7, K half m >> 3), and the diagonal blocks of D are the two
+// halves' partial sums -- 24 k-steps and 24 KiB of staged weights, not 48.
+#ifndef SPAI_LIN_HALVES
+#define SPAI_LIN_HALVES 1
+#endif
+constexpr int kLinHalves = SPAI_LIN_HALVES ? 2 : 1;
+constexpr int kLinBSteps = kLinKSteps / kLinHalves;   // B-fragment k-steps (staged, 1 KiB each)
 constexpr int kH = kY;                     // bf16 head features [8][kLinPitch] overlay Y
 constexpr int kHBytes = kP * 128;          // (all of Y)
 constexpr int kB = kH + kHBytes;           // 8 x (mine, theirs)
-constexpr int kL = kB + kS * 16;           // linear partials [4 waves][8][8] f32
+constexpr int kL = kB + kS * 16;           // linear partials [4 waves][halves][8][8] f32
 constexpr int kMaxBlocks = 20;
 constexpr int kBiasFloats = kHid + 2 * kMaxBlocks * kHid + kHid;   // stem, residual convs, head (64 padded)
-constexpr int kBias = kL + kWaves * 64 * 4; // all conv biases, staged once per workgroup
+constexpr int kBias = kL + kWaves * kLinHalves * 64 * 4; // all conv biases, staged once per workgroup
 constexpr int kPlanes = kBias + kBiasFloats * 4;   // stem neighbour planes [8][34] u64 (272-B rows: positions
                                                    // in different 16-B bank groups)
 constexpr int kPlaneRow = 34;
@@ -79,7 +89,7 @@ constexpr int kWStem = kPlanes + kS * kPlaneRow * 8;   // stem weight fragments 
 constexpr int kTab = kWStem + 4 * 64 * 16;         // k_geo_init: one S's row-group table [42] x 16 B (NetParams::geo)
 constexpr int kLinW = kTab + 42 * 16;             // the fused linear's B fragments [48 ks][64 lanes] x 16 B, staged
                                                    // once per launch by LDS-DMA (stage_linear)
-constexpr int kLdsBytes = kLinW + 48 * 1024;
+constexpr int kLdsBytes = kLinW + kLinBSteps * 1024;
 constexpr int kStamps = 24;                // phase stamps per wave in the diagnostic mode (17..19: inside block 0 conv1;
                                            // 20/21: s_memtime / s_memrealtime at kernel entry, 22: s_memrealtime at the
                                            // first group's stamp 0, 23: s_memrealtime after the last group)
@@ -785,8 +795,8 @@ __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const fl
 template <int W>
 __device__ __forceinline__ void stage_linear(uint8_t *smem, const NetParams &P, int lane) {
 #pragma unroll
-    for (int i = 0; i < kLinKSteps / kWaves; ++i) {
-        const int ks = W * (kLinKSteps / kWaves) + i;
+    for (int i = 0; i < kLinBSteps / kWaves; ++i) {
+        const int ks = W * (kLinBSteps / kWaves) + i;
         __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)(P.w_lin + ks * 64 + lane),
                                          (void __attribute__((address_space(3))) *)(smem + kLinW + ks * 1024), 16, 0, 0);
     }
@@ -834,9 +844,11 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
 // [12W, 12W+12) of 48 (B fragments from LDS, stage_linear); partial sums go to LDS.
 template <int W, int S>
 __device__ __forceinline__ void linear_mfma(uint8_t *smem, int lane) {
-    constexpr int k0 = (kLinKSteps / kWaves) * W, k1 = k0 + kLinKSteps / kWaves;
-    const int s = lane & 15, q = lane >> 4;
-    const uint8_t *hrow = s < S ? smem + kH + s * lin_pitch(S) * 2 + q * 16 : smem + kZ + q * 16;
+    constexpr int k0 = (kLinBSteps / kWaves) * W, k1 = k0 + kLinBSteps / kWaves;
+    const int m = lane & 15, q = lane >> 4;
+    // A row m: position m & 7 over K half m >> 3 (SPAI_LIN_HALVES), else position m
+    const int s = SPAI_LIN_HALVES ? (m & 7) : m, kh = SPAI_LIN_HALVES ? (m >> 3) : 0;
+    const uint8_t *hrow = s < S ? smem + kH + (s * lin_pitch(S) + kh * (kLinK / 2)) * 2 + q * 16 : smem + kZ + q * 16;
     const int hstep = s < S ? 64 : 0;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -845,10 +857,16 @@ __device__ __forceinline__ void linear_mfma(uint8_t *smem, int lane) {
         const uint4 b = *(const uint4 *)(smem + kLinW + ks * 1024 + lane * 16);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(b), acc, 0, 0, 0);
     }
-    float *L = (float *)(smem + kL) + W * 64;   // D[row s = 4q + r][col o = lane & 15]
-    if (q < 2 && (lane & 15) < 8) {
+    // D[row 4q + r][col n = lane & 15]
+    float *L = (float *)(smem + kL) + W * kLinHalves * 64;
+    if (SPAI_LIN_HALVES) {   // keep the diagonal blocks: row half (q >> 1) == column half (n >> 3)
+        if ((q >> 1) == (m >> 3)) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) L[(4 * q + r) * 8 + (lane & 15)] = acc[r];
+            for (int r = 0; r < 4; ++r) L[(q >> 1) * 64 + (4 * (q & 1) + r) * 8 + (m & 7)] = acc[r];
+        }
+    } else if (q < 2 && m < 8) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) L[(4 * q + r) * 8 + m] = acc[r];
     }
 }
 
@@ -988,7 +1006,11 @@ __device__ __forceinline__ void run_groups(uint8_t *smem, const NetParams &P, ui
             float sum8[8];
 #pragma unroll
             for (int o = 0; o < 8; ++o)
-                sum8[o] = L[tid * 8 + o] + L[64 + tid * 8 + o] + L[128 + tid * 8 + o] + L[192 + tid * 8 + o];
+                sum8[o] = 0.f;
+#pragma unroll
+            for (int pp = 0; pp < kWaves * kLinHalves; ++pp)   // fixed order: wave-major, K half
+#pragma unroll
+                for (int o = 0; o < 8; ++o) sum8[o] += L[pp * 64 + tid * 8 + o];
             float lg[c4::kActions];
             float mx = -INFINITY;
 #pragma unroll
@@ -1235,11 +1257,13 @@ int net_create(spai_engine *e, int blocks, int hidden, const float *params, size
     // fused linear as MFMA B fragments: [ks 48][lane 64][8], lane -> o = lane & 15,
     // k = ks*32 + 8*(lane>>4) + j over the head features H[s][cell*36 + c]; the
     // reference flattens c*42 + cell (policy c < 32 -> logits 0..6, value c = 32..34 -> o = 7)
-    std::vector<uint16_t> wlin((size_t)kLinKSteps * 64 * 8, 0);
-    for (int ks = 0; ks < kLinKSteps; ++ks)
+    // (SPAI_LIN_HALVES: [ks 24][lane 64][8], o = lane & 7, k = (lane >> 3 & 1) * 768 + ks*32 + ...)
+    std::vector<uint16_t> wlin((size_t)kLinBSteps * 64 * 8, 0);
+    for (int ks = 0; ks < kLinBSteps; ++ks)
         for (int l = 0; l < 64; ++l)
             for (int j = 0; j < 8; ++j) {
-                const int o = l & 15, k = ks * 32 + 8 * (l >> 4) + j;
+                const int o = SPAI_LIN_HALVES ? (l & 7) : (l & 15);
+                const int k = (SPAI_LIN_HALVES ? ((l >> 3) & 1) * (kLinK / 2) : 0) + ks * 32 + 8 * (l >> 4) + j;
                 const int cell = k / kHC, c = k % kHC;
                 float v = 0.f;
                 if (k < kLinFeat && o < 7 && c < 32) v = pol_w[(size_t)o * kPolIn + c * c4::kCells + cell];
