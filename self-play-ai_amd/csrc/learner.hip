@@ -106,6 +106,35 @@ __device__ __forceinline__ void stage_planes(const float *__restrict__ xb, int c
     }
 }
 
+// stage_planes without per-element index math: thread t < 252 owns cell t % 42
+// of channels t / 42 + 6j (source and LDS offsets are the thread's base plus
+// immediates), thread t < 240 zeroes border cell t % 30 of channels t / 30 + 8j;
+// the two sets are disjoint, so one barrier after the call covers both.
+template <int CINP>
+__device__ __forceinline__ void stage_planes_fast(const float *__restrict__ xb, int cin, float *xs) {
+    const int t = threadIdx.x;
+    if (t < 252) {
+        const int c0 = t / kCells, cell = t - c0 * kCells;
+        float *dst = xs + c0 * kPlane + (cell / kCols + 1) * 9 + cell % kCols + 1;
+        const float *src = xb + t;
+        float v[(CINP + 5) / 6];
+#pragma unroll
+        for (int j = 0; j < (CINP + 5) / 6; ++j) v[j] = c0 + 6 * j < cin ? src[252 * j] : 0.f;
+#pragma unroll
+        for (int j = 0; j < (CINP + 5) / 6; ++j)
+            if (c0 + 6 * j < CINP) dst[6 * kPlane * j] = v[j];
+    }
+    if (t < 240) {
+        const int c0 = t / 30, bi = t - c0 * 30;
+        const int k = bi - 18;
+        const int off = bi < 9 ? bi : bi < 18 ? 63 + bi - 9 : 9 * (1 + k / 2) + ((k & 1) ? 8 : 0);
+        float *dst = xs + c0 * kPlane + off;
+#pragma unroll
+        for (int j = 0; j < (CINP + 7) / 8; ++j)
+            if (c0 + 8 * j < CINP) dst[8 * kPlane * j] = 0.f;
+    }
+}
+
 // Wk[(tap * cinp + c) * coutp + n]: forward Wk = w[n][c][tap]; data gradient Wk = w[c][n][8 - tap].
 // Every conv's forward and data-gradient matrices are packed in one launch per
 // step (blockIdx.y = entry of the table built at learner_create):
@@ -150,7 +179,7 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
     float bq[PER];
 #pragma unroll
     for (int i = 0; i < PER; ++i) bq[i] = wl[(size_t)i * 4 * coutp_all];
-    stage_planes(in + (size_t)b * cin * kCells, cin, CINP, xs);
+    stage_planes_fast<CINP>(in + (size_t)b * cin * kCells, cin, xs);
     __syncthreads();
     // MTS = 3: the workgroup covers all 3 position tiles and blockIdx.y picks the
     // channel slice; MTS = 1: blockIdx.y picks the position tile (all channels)
