@@ -87,9 +87,15 @@ constexpr int kPlanes = kBias + kBiasFloats * 4;   // stem neighbour planes [8][
 constexpr int kPlaneRow = 34;
 constexpr int kWStem = kPlanes + kS * kPlaneRow * 8;   // stem weight fragments [4 ct][64 lanes] x 16 B, staged once
 constexpr int kTab = kWStem + 4 * 64 * 16;         // k_geo_init: one S's row-group table [42] x 16 B (NetParams::geo)
-constexpr int kLinW = kTab + 42 * 16;             // the fused linear's B fragments [48 ks][64 lanes] x 16 B, staged
-                                                   // once per launch by LDS-DMA (stage_linear)
-constexpr int kLdsBytes = kLinW + kLinBSteps * 1024;
+// The fused linear's B fragments: SPAI_LIN_REGS loads each wave's 6 k-steps
+// straight into registers at the head conv's start (no LDS copy); otherwise they
+// are staged in LDS at kLinW by LDS-DMA (stage_linear).
+#ifndef SPAI_LIN_REGS
+#define SPAI_LIN_REGS 1
+#endif
+constexpr int kLinW = kTab + 42 * 16;             // [24 ks][64 lanes] x 16 B (SPAI_LIN_REGS = 0)
+constexpr int kLinWPer = kLinBSteps / kWaves;      // B fragments per wave
+constexpr int kLdsBytes = kLinW + (SPAI_LIN_REGS ? 0 : kLinBSteps * 1024);
 constexpr int kStamps = 24;                // phase stamps per wave in the diagnostic mode (17..19: inside block 0 conv1;
                                            // 20/21: s_memtime / s_memrealtime at kernel entry, 22: s_memrealtime at the
                                            // first group's stamp 0, 23: s_memrealtime after the last group)
@@ -810,7 +816,8 @@ template <int W, int S, int DA>
 __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, int lane,
                                            const Geo<Plan<W, 4, npt_of(S)>::NT> &g,
                                            const int (&aux)[Plan<W, 4, npt_of(S)>::NT],
-                                           uint4 (&A)[DA][Plan<W, 4, npt_of(S)>::CTL]) {
+                                           uint4 (&A)[DA][Plan<W, 4, npt_of(S)>::CTL],
+                                           uint4 (&wlin)[kLinWPer]) {
     constexpr int NPT = npt_of(S);
     using PL = Plan<W, 4, NPT>;
     int hoff[PL::NT];   // head-feature offset of each tile's row (-1: padding)
@@ -819,7 +826,12 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
         const int s = aux[t] & 255, b = aux[t] >> 8;   // b = col*7 + row
         hoff[t] = s < S ? s * lin_pitch(S) + ((b % c4::kCols) * c4::kCols + b / c4::kCols) * kHC : -1;
     }
-    stage_linear<W>(smem, P, lane);
+    if (SPAI_LIN_REGS) {   // this wave's linear B fragments, consumed after the head conv
+#pragma unroll
+        for (int i = 0; i < kLinWPer; ++i) wlin[i] = P.w_lin[(W * kLinWPer + i) * 64 + lane];
+    } else {
+        stage_linear<W>(smem, P, lane);
+    }
     f32x4 acc[PL::n];
     conv_mfma<W, 4, NPT, S, kX, DA, b_depth(S), 3, kH>(smem, g, (const float *)(smem + kBias) + kHid * (1 + 2 * P.blocks),
                                                       P.w_head, P.w_head, lane, A, acc, hoff);
@@ -843,7 +855,7 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
 // 1344 <= k < 1470; connect_four.rs:63-64,69-70).  Wave W takes k-steps
 // [12W, 12W+12) of 48 (B fragments from LDS, stage_linear); partial sums go to LDS.
 template <int W, int S>
-__device__ __forceinline__ void linear_mfma(uint8_t *smem, int lane) {
+__device__ __forceinline__ void linear_mfma(uint8_t *smem, int lane, const uint4 (&wlin)[kLinWPer]) {
     constexpr int k0 = (kLinBSteps / kWaves) * W, k1 = k0 + kLinBSteps / kWaves;
     const int m = lane & 15, q = lane >> 4;
     // A row m: position m & 7 over K half m >> 3 (SPAI_LIN_HALVES), else position m
@@ -854,7 +866,7 @@ __device__ __forceinline__ void linear_mfma(uint8_t *smem, int lane) {
 #pragma unroll
     for (int ks = k0; ks < k1; ++ks) {
         const uint4 a = *(const uint4 *)(hrow + ks * hstep);
-        const uint4 b = *(const uint4 *)(smem + kLinW + ks * 1024 + lane * 16);
+        const uint4 b = SPAI_LIN_REGS ? wlin[ks - k0] : *(const uint4 *)(smem + kLinW + ks * 1024 + lane * 16);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(b), acc, 0, 0, 0);
     }
     // D[row 4q + r][col n = lane & 15]
@@ -923,11 +935,12 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
         if (l2 < 12) stamp(P, W, lane, 2 + l2);
     }
     if (kDiagHead) stamp(P, W, lane, 19);   // diagnostic head mode: 19 = before the head, 17 = head k-loop, 18 = H written
-    head_layer<W, S, DA>(smem, P, lane, g, aux, A);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stage_linear copies have landed
+    uint4 wlin[kLinWPer];
+    head_layer<W, S, DA>(smem, P, lane, g, aux, A, wlin);
+    if (!SPAI_LIN_REGS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stage_linear copies have landed
     __syncthreads();
     stamp(P, W, lane, 14);
-    linear_mfma<W, S>(smem, lane);
+    linear_mfma<W, S>(smem, lane, wlin);
 }
 
 // Group size for `count` leaves on `grid` workgroups: the fewest rounds R of at
