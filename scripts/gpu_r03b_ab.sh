@@ -11,11 +11,13 @@ fi
 if [ -n "${PHASES:-}" ]; then
   SPAI_LIB=$PWD/build_exp/libspai_diag.so timeout -k 10 300 python scripts/net_phases.py > $O/phases.txt 2>&1; rc=$?; tail -9 $O/phases.txt; [ $rc -eq 0 ] || exit $rc
 fi
+if [ -n "${FWD:-}" ]; then
 LIBS=$(for v in $FWD; do printf "build_exp/libspai_$v.so,"; done); LIBS=${LIBS%,}
-for r in 1 2; do
-  timeout -k 10 300 python scripts/fwd_sweep.py --libs $LIBS --counts ${COUNTS:-256,512,1006,1536,2048,4096} > $O/sweep_$r.txt 2>&1 || { cat $O/sweep_$r.txt; exit 1; }
-  cat $O/sweep_$r.txt
-done
+  for r in 1 2; do
+    timeout -k 10 300 python scripts/fwd_sweep.py --libs $LIBS --counts ${COUNTS:-256,512,1006,1536,2048,4096} > $O/sweep_$r.txt 2>&1 || { cat $O/sweep_$r.txt; exit 1; }
+    cat $O/sweep_$r.txt
+  done
+fi
 for r in 1 2; do
   for v in $BENCHV; do
     SPAI_LIB=$PWD/build_exp/libspai_$v.so timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-isolated > $O/bench_${v}_$r.json 2> $O/bench_${v}_$r.err || { tail -5 $O/bench_${v}_$r.err; exit 1; }
