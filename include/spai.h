@@ -179,10 +179,7 @@ int spai_tree_size(spai_engine *eng, uint32_t tree, uint32_t *nodes);
  * probability proportional to N^temperature, record (root state, visit policy),
  * and when the sampled child is terminal emit the game's samples with the value
  * signed per player to move (:211-225).  The sink is called once per finished
- * game, in the reference's emission order.  spai_selfplay_run (Connect4) calls it
- * from one helper thread of its own, never concurrently, while the next move's
- * search runs on the device; every call has returned before spai_selfplay_run
- * does. */
+ * game, in the reference's emission order. */
 typedef void (*spai_sample_sink)(void *user, uint32_t game_id, uint32_t n, const float *encodings /* [n][3*6*7] */,
                                  const float *policies /* [n][7] */, const float *values /* [n] */,
                                  const int32_t *moves /* [n] action played at each position */);
