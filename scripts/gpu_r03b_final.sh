@@ -21,3 +21,11 @@ for c in FETCH_SIZE WRITE_SIZE; do
   rc=$?; echo "pass $c rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/traffic_bench_$c.err; exit $rc; }
 done
 python3 scripts/pmc_summary.py $O/forward_traffic.json $(find /tmp/pmc_FETCH_SIZE /tmp/pmc_WRITE_SIZE -name '*counter_collection*.csv') && grep -A5 '"k_forward<false>"' $O/forward_traffic.json
+if [ -n "${LV:-}" ]; then
+  for r in 1 2; do
+    for v in $LV; do
+      SPAI_LIB=$PWD/build_exp/libspai_$v.so timeout -k 10 200 python scripts/learner_dp.py --steps 200 > $O/learner_${v}_$r.json 2> $O/learner_${v}_$r.err || { tail -3 $O/learner_${v}_$r.err; exit 1; }
+      python3 -c "import json;d=json.load(open('$O/learner_${v}_$r.json'));print('== $v $r', round(d['value']), 'samples/s', round(d['ms_per_step'],3), 'ms/step')"
+    done
+  done 2>&1 | tee $O/learner_variants.txt
+fi
