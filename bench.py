@@ -15,9 +15,18 @@ process never imports torch (torch ships its own HIP runtime with the same
 SONAME).
 
 Adds to the JSON line:
-  roofline      the fused forward kernel (dominant): algorithmic FLOPs of the
-                evaluated leaves / HIP-event time of the sampled launches
-                (engine stream), vs the 2.5 PF dense bf16 MFMA peak
+  roofline      the fused forward kernel (dominant) vs the 2.5 PF dense bf16
+                MFMA peak.  achieved/frac = job level: the algorithmic FLOPs of
+                every leaf evaluated in the timed region over its wall time (the
+                two search chains' forwards overlap each other and the tree
+                kernels, so per-launch event times overlap and do not add up to
+                the step).  per_launch = the same FLOPs over the HIP-event time
+                of the sampled launches (engine streams; CUs shared), the figure
+                rocprof's kernel average checks.  isolated = the kernel alone.
+  rules_kernels the bitboard rules kernels (k_legal4, k_apply4, k_encode bf16)
+                on 2^24 game slots: algorithmic bytes / HIP-event time vs 8 TB/s
+  chess         BASELINE config 4 window: 1024 chess games x 400 sims, the
+                first 2 moves (sims/s, k_chess_forward fraction of peak)
   cpu_baseline  the CPU restatement (oracle/refcpu.py: reference data layout,
                 AoS arena with State clones, sequential tree loop) with the net
                 on libtorch CPU fp32, run in a subprocess: a small batch of games
@@ -67,7 +76,9 @@ def parse():
                     help="games the CPU baseline plays to completion inside this run (~45 s on the GPU box's host)")
     ap.add_argument("--cpu-timeout", type=float, default=240.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--rules-bench", action="store_true", help="also time the batched rules kernels")
+    ap.add_argument("--no-rules-bench", action="store_true", help="skip the batched rules-kernel timing (HBM GB/s)")
+    ap.add_argument("--no-chess", action="store_true", help="skip the chess window (config 4, 2 moves)")
+    ap.add_argument("--chess-moves", type=int, default=2)
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events (A/B of their cost)")
     ap.add_argument("--no-isolated", action="store_true", help="skip the isolated-forward measurement")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r03", "final_b2", "forward_traffic.json"),
@@ -165,6 +176,67 @@ class Dist:
         self.g.close()
 
 
+def rules_bench(eng):
+    """k_legal4 / k_apply4 / k_encode<bf16> over 2^24 C4 game slots (spai_rules_bench:
+    HIP events over 10 launches each); algorithmic bytes per slot: legal 16 B of
+    bitboards in + 2 B mask out, apply 16 + 1 + 4 (action) in and 8 + 4 out, encode
+    16 B in + 126 x 2 B planes + 1 out"""
+    n = 1 << 24
+    ms = eng.rules_bench(n, iters=10)
+    out = {}
+    for nm, m, b in zip(("k_legal4", "k_apply4", "k_encode_bf16"), ms, (18, 33, 269)):
+        gbs = n * b / (m * 1e-3) / 1e9
+        out[nm] = {"ms": m, "slots": n, "bytes_per_slot": b, "GB/s": gbs, "frac": gbs / HBM_PEAK_GBS}
+    return out
+
+
+def chess_window(args, device):
+    """BASELINE config 4 (chess, 1024 games x 400 sims/move, 20x256 bf16) for the first
+    --chess-moves moves from the start position: every move searches every live tree,
+    samples visits^1.25 and re-roots (scripts/chess_bench.py, windowed).  sims/s and
+    k_chess_forward's algorithmic FLOPs over its HIP-event time; ~2 s of GPU time"""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "scripts"))
+    import chess_bench as cb
+    import spai_chess as sc
+    games, sims, blocks = 1024, 400, 20
+    eng = sc.ChessEngine(num_searches=sims, max_trees=games, eval_kind=sc.EVAL_NET, device=device, seed=args.seed)
+    net = sc.ChessNet(eng, blocks, sc.init_params(blocks, args.seed))
+    eng.set_net(net)
+    eng.trees_create(games)
+    eng.search(np.arange(games), num_searches=4)   # warm-up
+    eng.trees_create(games)
+    eng.set_timing(True)
+    rng = np.random.default_rng(args.seed)
+    live = np.arange(games, dtype=np.uint32)
+    done = 0
+    t0 = time.perf_counter()
+    for _ in range(args.chess_moves):
+        _, _, vis, _, nc = eng.search(live)
+        done += len(live) * sims
+        w = np.power(vis.astype(np.float64), 1.25)   # learner_concurrent.rs:189-193
+        w[np.arange(vis.shape[1])[None, :] >= nc[:, None]] = 0
+        cum = np.cumsum(w, 1)
+        u = rng.random(len(live))[:, None] * cum[:, -1:]
+        pick = np.minimum((cum <= u).sum(1), nc - 1).astype(np.uint32)
+        status, _ = eng.advance(live, pick)
+        live = live[status == 0]
+    dt = time.perf_counter() - t0
+    ms, launches, items = eng.timing()
+    net.close()
+    eng.close()
+    fpe = cb.flops_per_eval(blocks)
+    leaves = items[1] / max(1.0, launches[1])
+    tf = fpe * leaves / (ms[1] * 1e-3) / 1e12 if ms[1] > 0 else None
+    return {"workload": "chess self-play, %d games x %d sims/move, %dx256 ResNet bf16, first %d moves from the "
+                        "start position" % (games, sims, blocks, args.chess_moves),
+            "sims_per_sec": done / dt, "seconds": dt,
+            "forward": {"kernel": "k_chess_forward", "avg_launch_ms": ms[1], "avg_leaves_per_launch": leaves,
+                        "flop_per_eval": fpe, "achieved_TFLOP/s": tf,
+                        "frac": tf / BF16_PEAK_TFLOPS if tf else None},
+            "kernel_ms": {"select_leaf": ms[0], "forward": ms[1], "expand": ms[2]}}
+
+
 def main():
     args = parse()
     if args.cpu_baseline_only:
@@ -239,18 +311,25 @@ def main():
         "positions_per_sec": positions / dt_max,
         "kernel_ms": {k: v["avg_ms"] for k, v in timing.items()},
         "roofline": {"bound": "mfma", "kernel": "k_forward (fused 6x64 ResNet)",
-                     "achieved": achieved, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / BF16_PEAK_TFLOPS if achieved else None, "traffic": traffic,
+                     # job level: every forward FLOP of the timed region over its wall time
+                     "achieved": evals / dt_max * fpe / 1e12 / dist.world, "peak": BF16_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": evals / dt_max * fpe / 1e12 / dist.world / BF16_PEAK_TFLOPS,
+                     "basis": "job level: flop_per_eval x leaves evaluated in the timed region / its wall time, "
+                              "per GPU (the two search chains' forwards overlap, so per-launch event times "
+                              "over-count the step; see per_launch)",
+                     "traffic": traffic,
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                      # algorithmic bytes of one launch: the packed bf16 weights + fp32 biases once,
                      # plus per leaf 16 B of bitboards in and 36 B (8 priors + value) out
                      "algorithmic_bytes": weight_bytes(args.blocks) + 52 * (ev["items"] / max(1, ev["launches"])),
                      "flop_per_launch": per_launch_flop, "flop_per_eval": fpe,
-                     # whole-GPU view: every forward FLOP of the timed region over its wall time
-                     # (the two search chains' forwards overlap, so this is not per launch)
-                     "chip_achieved": evals / dt_max * fpe / 1e12 / dist.world,
-                     "chip_frac": evals / dt_max * fpe / 1e12 / dist.world / BF16_PEAK_TFLOPS,
-                     "avg_launch_ms": ev["avg_ms"], "avg_leaves_per_launch": ev["items"] / max(1, ev["launches"])},
+                     "avg_launch_ms": ev["avg_ms"], "avg_leaves_per_launch": ev["items"] / max(1, ev["launches"]),
+                     # per launch: HIP events on the chain streams (every 32nd iteration); the
+                     # CUs are shared with the other chain's kernels while a launch runs
+                     "per_launch": {"achieved": achieved,
+                                    "frac": achieved / BF16_PEAK_TFLOPS if achieved else None,
+                                    "avg_launch_ms": ev["avg_ms"], "launches_sampled": ev["launches"],
+                                    "note": "shared CUs: launches x avg_launch_ms exceeds the step time"}},
     }
     # the same forward launch ALONE on the GPU (spai_net_bench, HIP events, random reachable
     # positions) at the timed region's mean leaves per launch, at one chain's (x2) and at the
@@ -268,12 +347,15 @@ def main():
                                                "300 back-to-back launches between HIP events, after ~0.2 s of "
                                                "warm-up launches); the timed region's per-launch figure shares the "
                                                "CUs with the other search chain")
-    if args.rules_bench and dist.rank == 0:
-        n = 1 << 24
-        ms = eng.rules_bench(n, iters=10)
-        bytes_per = [18, 33, 269]
-        result["rules_kernels"] = {nm: {"ms": m, "GB/s": n * b / (m * 1e-3) / 1e9, "frac": n * b / (m * 1e-3) / 1e9 / HBM_PEAK_GBS}
-                                   for nm, m, b in zip(("legal", "apply", "encode_bf16"), ms, bytes_per)}
+    if not args.no_rules_bench and dist.rank == 0:
+        result["rules_kernels"] = rules_bench(eng)
+    net.close()
+    eng.close()
+    if not args.no_chess and dist.rank == 0:
+        try:
+            result["chess"] = chess_window(args, dist.local)
+        except Exception as ex:   # the window must never sink the headline number
+            result["chess"] = {"error": repr(ex)[:300]}
     net.close()
     eng.close()
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:

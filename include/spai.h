@@ -35,7 +35,7 @@ extern "C" {
 #endif
 
 #define SPAI_VERSION_MAJOR 0
-#define SPAI_VERSION_MINOR 1
+#define SPAI_VERSION_MINOR 2
 
 typedef enum spai_error {
     SPAI_OK = 0,
@@ -276,6 +276,21 @@ int spai_learner_set_comm(spai_learner *l, int rank, int world, const uint8_t *i
  * trainer's weights to the self-play workers): RCCL broadcast of rank `root`'s parameters
  * to every rank of the communicator; a learner without one is left unchanged. */
 int spai_learner_broadcast(spai_learner *l, int root);
+/* Host collective in place of RCCL, for ranks that cannot form an RCCL
+ * communicator (several ranks on one device, a host process group):
+ * fn(user, buf, n) must sum the n floats of buf element-wise over the `world`
+ * ranks in place (the same rank order on every rank, so the replicas stay
+ * bit-identical) and return 0.  The step runs the same batch-size weighting and
+ * running-statistic averaging as with RCCL; each all-reduce is staged through
+ * pinned host memory and the call blocks in fn until every rank has arrived.
+ * spai_learner_broadcast then sums rank `root`'s parameters with -0.0 from every
+ * other rank (x + -0.0 == x for every x).  fn NULL (or world 1) drops it;
+ * setting one drops an RCCL communicator and vice versa. */
+typedef int (*spai_host_allreduce)(void *user, float *buf, size_t n);
+int spai_learner_set_host_comm(spai_learner *l, int rank, int world, spai_host_allreduce fn, void *user);
+/* the batch size of the latest train step (0 before the first); after
+ * spai_learner_train it is the last minibatch's (n % batch, or batch) */
+int spai_learner_last_batch(spai_learner *l, uint32_t *n);
 
 /* ---------------------------------------------------------------- checkpoints
  * safetensors files with tch VarStore naming (VarStore::save / load,
@@ -321,7 +336,10 @@ int spai_choose_multiple(uint32_t n, uint32_t k, uint64_t seed, uint64_t stream,
  * and the weight version its games were played with; a POP event carries the
  * batch the trainer took for one train step and the number of weight versions
  * published so far.  Tests replay the events through a HeapRb model.  The
- * callback must not call back into the pipeline. */
+ * callback must not call back into the pipeline.  It runs while the ring's lock
+ * is held, so every self-play worker and the trainer wait for it: it must be
+ * fast and must not block (copy what it needs and return); run timings with an
+ * observer are not representative. */
 enum { SPAI_PIPE_PUSH = 0, SPAI_PIPE_POP = 1 };
 typedef struct spai_pipeline_event {
     int32_t kind;          /* SPAI_PIPE_PUSH / SPAI_PIPE_POP */
@@ -336,6 +354,12 @@ typedef struct spai_pipeline_event {
 } spai_pipeline_event;
 typedef void (*spai_pipeline_observer)(void *user, const spai_pipeline_event *ev);
 typedef struct spai_pipeline_config {
+    /* ABI guard: the caller sets struct_size = sizeof(spai_pipeline_config) before
+     * spai_pipeline_config_default / spai_pipeline_run; a size the library was not
+     * built with (a client compiled against another header) is refused with
+     * SPAI_ERR_INVALID before anything is read or written (added in 0.2 with the
+     * observer fields) */
+    uint32_t struct_size;
     uint32_t n_selfplay;
     const int *selfplay_devices;   /* [n_selfplay] */
     int learner_device;

@@ -82,6 +82,49 @@ def train_step(params, adam_m, adam_v, step, x, pi, z, blocks, hidden, lr=1e-3, 
     (pre-activation > 0) — e.g. the device step's own (post-ReLU activation > 0), so
     that a pre-activation within rounding of 0 takes the same side of the kink in
     both.  diag: optional dict that receives the pre-activations ("pre", per layer)."""
+    P, G, loss = forward_backward(params, x, pi, z, blocks, hidden, momentum, bn_eps, masks, diag)
+    P, m, vv = adam(P, G, adam_m, adam_v, step, lr, b1, b2, eps)
+    return P, m, vv, loss, G
+
+
+def adam(P, G, adam_m, adam_v, step, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8):
+    """Adam (running statistics have zero gradient, so their moments stay 0 and they are not moved)"""
+    m = b1 * np.asarray(adam_m, np.float64) + (1 - b1) * G
+    vv = b2 * np.asarray(adam_v, np.float64) + (1 - b2) * G * G
+    t = step + 1
+    P = P - (lr / (1 - b1 ** t)) * m / (np.sqrt(vv) / np.sqrt(1 - b2 ** t) + eps)
+    return P, m, vv
+
+
+def train_step_dp(params, adam_m, adam_v, step, rank_batches, blocks, hidden, lr=1e-3, b1=0.9, b2=0.999,
+                  eps=1e-8, momentum=0.1, bn_eps=1e-5, rank_masks=None, rank_diags=None):
+    """one data-parallel optimizer step over len(rank_batches) ranks, as DDP without
+    SyncBN (the distribution learner_concurrent.rs:72-85 would get from torch DDP):
+    every rank runs the train-mode forward/backward on its own batch (its own BN
+    batch statistics, its own running-statistic update), the step's gradient is the
+    mean over the union of the batches, sum_r (B_r / sum B) * g_r, one Adam step on
+    it, and the running statistics are the ranks' updated ones averaged.  Returns
+    (params, m, v, per-rank losses, the reduced gradient, per-rank gradients)."""
+    parts = []
+    for r, (x, pi, z) in enumerate(rank_batches):
+        parts.append(forward_backward(params, x, pi, z, blocks, hidden, momentum, bn_eps,
+                                      None if rank_masks is None else rank_masks[r],
+                                      None if rank_diags is None else rank_diags[r]))
+    sizes = np.array([len(np.asarray(b[2]).reshape(-1)) for b in rank_batches], np.float64)
+    G = sum((sizes[r] / sizes.sum()) * parts[r][1] for r in range(len(parts)))
+    convs, _, _ = _layout(blocks, hidden)
+    P = np.asarray(parts[0][0], np.float64).copy()
+    for c in convs:   # running statistics: the mean of the ranks' updated values
+        for key in ("mu", "var"):
+            sl = slice(c[key], c[key] + c["co"])
+            P[sl] = np.mean([p[0][sl] for p in parts], axis=0)
+    P, m, vv = adam(P, G, adam_m, adam_v, step, lr, b1, b2, eps)
+    return P, m, vv, [p[2] for p in parts], G, [p[1] for p in parts]
+
+
+def forward_backward(params, x, pi, z, blocks, hidden, momentum=0.1, bn_eps=1e-5, masks=None, diag=None):
+    """train-mode forward + backward of one batch; returns (params with the BN running
+    statistics updated, gradients, loss[3]) — float64"""
     convs, lin, n = _layout(blocks, hidden)
     P = np.asarray(params, np.float64).copy()
     G = np.zeros(n)
@@ -166,12 +209,7 @@ def train_step(params, adam_m, adam_v, step, x, pi, z, blocks, hidden, lr=1e-3, 
         dr1 = bn_conv_bwd(l2, dt)
         dh = dt + bn_conv_bwd(l1, dr1)
     bn_conv_bwd(0, dh, want_dx=False)
-    # Adam (running statistics have zero gradient, so their moments stay 0 and they are not moved)
-    m = b1 * np.asarray(adam_m, np.float64) + (1 - b1) * G
-    vv = b2 * np.asarray(adam_v, np.float64) + (1 - b2) * G * G
-    t = step + 1
-    P = P - (lr / (1 - b1 ** t)) * m / (np.sqrt(vv) / np.sqrt(1 - b2 ** t) + eps)
-    return P, m, vv, np.array([lp + lv, lp, lv]), G
+    return P, G, np.array([lp + lv, lp, lv])
 
 
 def train(params, batches, blocks, hidden, **kw):

@@ -55,7 +55,7 @@ def main():
     local = int(os.environ.get("SPAI_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
     uid = g.broadcast_bytes(spai.comm_unique_id() if rank == 0 else None) if world > 1 else spai.comm_unique_id()
     R = Config3Rank(rank, world, uid, games=a.games, sims=a.sims, blocks=a.blocks, batch=a.batch,
-                    train_steps=a.train_steps, fraction=a.fraction, seed=a.seed, device=local)
+                    train_steps=a.train_steps, fraction=a.fraction, seed=a.seed, device=local, group=g)
     loss = None
     g.barrier()
     t_all = time.perf_counter()
@@ -76,7 +76,8 @@ def main():
             "n_gpus": world, "rounds": a.rounds,
             "selfplay_sims_per_sec": sims / sp_max, "selfplay_games_per_sec": ngames / sp_max,
             "positions": pos, "train_samples_per_sec": samples / tr_max if tr_max > 0 else None,
-            "train_steps_per_round": a.train_steps, "batch_per_rank": a.batch,
+            "train_steps_per_round": a.train_steps, "steps_trained": tot["steps_trained"],
+            "steps_skipped": tot["steps_skipped"], "batch_per_rank": a.batch,
             "seconds": {"selfplay": sp_max, "train": tr_max, "refresh": rf_max, "wall": wall_max},
             "collectives": "RCCL all-reduce of %d fp32 gradients per train step; RCCL broadcast of the "
                            "parameters per round" % R.learner.n,

@@ -106,7 +106,7 @@ extern "C" {
 
 const char *spai_last_error(void) { return g_err; }
 
-const char *spai_version(void) { return "spai 0.1 (gfx950)"; }
+const char *spai_version(void) { return "spai 0.2 (gfx950)"; }
 
 int spai_device_count(int *count) {
     PTR_CHECK(count);
@@ -469,6 +469,19 @@ int spai_learner_broadcast(spai_learner *l, int root) {
     return learner_broadcast(l, root);
 }
 
+int spai_learner_set_host_comm(spai_learner *l, int rank, int world, spai_host_allreduce fn, void *user) {
+    PTR_CHECK(l);
+    ENG_CHECK(l->eng);
+    return learner_set_host_comm(l, rank, world, fn, user);
+}
+
+int spai_learner_last_batch(spai_learner *l, uint32_t *n) {
+    PTR_CHECK(l);
+    PTR_CHECK(n);
+    *n = l->last_batch;
+    return SPAI_OK;
+}
+
 // ---------------------------------------------------------------- checkpoints
 int spai_params_save_safetensors(int game, int blocks, int hidden, const float *params, size_t n, const char *path) {
     PTR_CHECK(params);
@@ -527,10 +540,18 @@ int spai_choose_multiple(uint32_t n, uint32_t k, uint64_t seed, uint64_t stream,
     return SPAI_OK;
 }
 
+#define PIPE_CFG_CHECK(cfg)                                                                                  \
+    SPAI_CHECK((cfg)->struct_size == sizeof(spai_pipeline_config), SPAI_ERR_INVALID,                        \
+               "spai_pipeline_config.struct_size is %u, this library expects %zu (set it to "                \
+               "sizeof(spai_pipeline_config) of the header the library was built with)",                   \
+               (unsigned)(cfg)->struct_size, sizeof(spai_pipeline_config))
+
 int spai_pipeline_config_default(spai_pipeline_config *cfg) {
     PTR_CHECK(cfg);
+    PIPE_CFG_CHECK(cfg);
     static const int dev0 = 0;
     *cfg = spai_pipeline_config{};
+    cfg->struct_size = sizeof(spai_pipeline_config);
     cfg->n_selfplay = 1;
     cfg->selfplay_devices = &dev0;
     cfg->learner_device = 0;
@@ -552,6 +573,7 @@ int spai_pipeline_config_default(spai_pipeline_config *cfg) {
 int spai_pipeline_run(const spai_pipeline_config *cfg, const float *init_params, size_t n_params,
                       spai_pipeline_stats *stats) {
     PTR_CHECK(cfg);
+    PIPE_CFG_CHECK(cfg);
     PTR_CHECK(init_params);
     return pipeline_run(cfg, init_params, n_params, stats);
 }

@@ -899,6 +899,7 @@ void learner_destroy(spai_learner *L) {
     }
     L->pack_desc.release();
     if (L->stage) (void)hipHostFree(L->stage);
+    if (L->host_buf) (void)hipHostFree(L->host_buf);
     for (auto *b : {&L->p, &L->g, &L->bsum, &L->m, &L->v, &L->wt, &L->batch_in, &L->d0, &L->d1, &L->dlogits,
                     &L->dpre, &L->loss_terms, &L->run_buf})
         b->release();
@@ -906,6 +907,26 @@ void learner_destroy(spai_learner *L) {
     for (auto *vec : {&L->z, &L->a, &L->mean, &L->invstd})
         for (auto &b : *vec) b.release();
     delete L;
+}
+
+// One cross-rank sum of n device floats, in place, in stream order: RCCL over
+// xGMI, or the caller's host collective (spai_learner_set_host_comm) through the
+// pinned staging buffer, which blocks the calling thread until every rank arrived.
+static int learner_allreduce(spai_learner *L, float *buf, size_t n, hipStream_t st, const char *what) {
+    if (L->comm) {
+        if (ncclAllReduce(buf, buf, n, ncclFloat32, ncclSum, (ncclComm_t)L->comm, st) != ncclSuccess) {
+            set_error("ncclAllReduce of %s failed", what);
+            return SPAI_ERR_DEVICE;
+        }
+        return SPAI_OK;
+    }
+    SPAI_CHECK(L->host_ar && n <= L->host_buf_n, SPAI_ERR_INVALID, "host all-reduce of %s: no collective", what);
+    SPAI_HIP(hipMemcpyAsync(L->host_buf, buf, n * 4, hipMemcpyDeviceToHost, st));
+    SPAI_HIP(hipStreamSynchronize(st));
+    const int r = L->host_ar(L->host_ar_user, L->host_buf, n);
+    SPAI_CHECK(r == 0, SPAI_ERR_DEVICE, "host all-reduce of %s failed (%d)", what, r);
+    SPAI_HIP(hipMemcpyAsync(buf, L->host_buf, n * 4, hipMemcpyHostToDevice, st));
+    return SPAI_OK;
 }
 
 // Everything of one train step after the batch upload: gradients zeroed, weights
@@ -1010,27 +1031,19 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
     // then the gradients are summed.  Exact for unequal per-rank batches; a 1-rank
     // communicator multiplies by 1 and reduces to a copy (bit-identical step).
     const float gscale = 1.0f;
-    if (L->comm) {
+    const bool dp = L->comm || L->host_ar;
+    if (dp) {
         k_set1<<<1, 1, 0, st>>>(L->bsum.p, (float)B);
-        if (ncclAllReduce(L->bsum.p, L->bsum.p, 1, ncclFloat32, ncclSum, (ncclComm_t)L->comm, st) != ncclSuccess) {
-            set_error("ncclAllReduce of the batch sizes failed");
-            return SPAI_ERR_DEVICE;
-        }
+        SPAI_TRY(learner_allreduce(L, L->bsum.p, 1, st, "the batch sizes"));
         k_weight_grad<<<blocks_of(L->n_params), kThreads, 0, st>>>(G, L->n_params, (float)B, L->bsum.p);
-        if (ncclAllReduce(G, G, L->n_params, ncclFloat32, ncclSum, (ncclComm_t)L->comm, st) != ncclSuccess) {
-            set_error("ncclAllReduce of the gradients failed");
-            return SPAI_ERR_DEVICE;
-        }
+        SPAI_TRY(learner_allreduce(L, G, L->n_params, st, "the gradients"));
     }
     k_adam<<<blocks_of(L->n_params), kThreads, 0, st>>>(P, G, L->m.p, L->v.p, L->n_params, gscale, L->cfg.lr,
                                                         L->cfg.beta1, L->cfg.beta2, L->cfg.eps, bc);
-    if (L->comm) {   // average the BN running statistics so replicas stay identical
+    if (dp) {   // average the BN running statistics so replicas stay identical
         const uint32_t nr = (uint32_t)L->run_idx.n;
         k_gather<<<blocks_of(nr), kThreads, 0, st>>>(P, L->run_idx.p, nr, L->run_buf.p);
-        if (ncclAllReduce(L->run_buf.p, L->run_buf.p, nr, ncclFloat32, ncclSum, (ncclComm_t)L->comm, st) != ncclSuccess) {
-            set_error("ncclAllReduce of the BN running statistics failed");
-            return SPAI_ERR_DEVICE;
-        }
+        SPAI_TRY(learner_allreduce(L, L->run_buf.p, nr, st, "the BN running statistics"));
         k_scatter_scaled<<<blocks_of(nr), kThreads, 0, st>>>(L->run_buf.p, L->run_idx.p, nr, 1.0f / (float)L->world, P);
     }
     SPAI_HIP(hipGetLastError());
@@ -1131,6 +1144,8 @@ int learner_set_comm(spai_learner *L, int rank, int world, const uint8_t *id) {
         (void)ncclCommDestroy((ncclComm_t)L->comm);
         L->comm = nullptr;
     }
+    L->host_ar = nullptr;   // an RCCL communicator (or none) replaces a host collective
+    L->host_ar_user = nullptr;
     L->rank = rank;
     L->world = world;
     if (!id) return SPAI_OK;   // world == 1 without an id: no communicator
@@ -1149,13 +1164,54 @@ int learner_set_comm(spai_learner *L, int rank, int world, const uint8_t *id) {
 // statistics included) become rank `root`'s, by one RCCL broadcast over xGMI
 int learner_broadcast(spai_learner *L, int root) {
     SPAI_CHECK(root >= 0 && root < L->world, SPAI_ERR_INVALID, "broadcast root %d outside world %d", root, L->world);
-    if (!L->comm) return SPAI_OK;   // no communicator: a single replica
     hipStream_t st = L->eng->stream;
+    if (L->host_ar) {   // rank root's values plus -0.0 from every other rank: x + -0.0 == x exactly
+        SPAI_HIP(hipStreamSynchronize(st));
+        if (L->rank == root) {
+            SPAI_HIP(hipMemcpy(L->host_buf, L->p.p, L->n_params * 4, hipMemcpyDeviceToHost));
+        } else {
+            for (size_t i = 0; i < L->n_params; ++i) L->host_buf[i] = -0.0f;
+        }
+        const int r = L->host_ar(L->host_ar_user, L->host_buf, L->n_params);
+        SPAI_CHECK(r == 0, SPAI_ERR_DEVICE, "host all-reduce of the parameters failed (%d)", r);
+        SPAI_HIP(hipMemcpy(L->p.p, L->host_buf, L->n_params * 4, hipMemcpyHostToDevice));
+        return SPAI_OK;
+    }
+    if (!L->comm) return SPAI_OK;   // no communicator: a single replica
     if (ncclBroadcast(L->p.p, L->p.p, L->n_params, ncclFloat32, root, (ncclComm_t)L->comm, st) != ncclSuccess) {
         set_error("ncclBroadcast of the parameters failed");
         return SPAI_ERR_DEVICE;
     }
     SPAI_HIP(hipStreamSynchronize(st));
+    return SPAI_OK;
+}
+
+// host collective in place of RCCL (the same step, each all-reduce staged through pinned memory)
+int learner_set_host_comm(spai_learner *L, int rank, int world, spai_host_allreduce fn, void *user) {
+    SPAI_CHECK(world >= 1 && rank >= 0 && rank < world, SPAI_ERR_INVALID, "bad rank %d / world %d", rank, world);
+    if (L->comm) {
+        (void)ncclCommDestroy((ncclComm_t)L->comm);
+        L->comm = nullptr;
+    }
+    L->rank = fn ? rank : 0;
+    L->world = fn ? world : 1;
+    L->host_ar = fn;
+    L->host_ar_user = user;
+    if (!fn) return SPAI_OK;
+    const size_t need = std::max(L->n_params, L->run_idx.n);
+    if (L->host_buf_n < need) {
+        if (L->host_buf) (void)hipHostFree(L->host_buf);
+        L->host_buf = nullptr;
+        L->host_buf_n = 0;
+        if (hipHostMalloc((void **)&L->host_buf, need * sizeof(float), hipHostMallocDefault) != hipSuccess) {
+            L->host_buf = nullptr;
+            L->host_ar = nullptr;
+            L->world = 1;
+            set_error("learner: pinned host-collective buffer allocation failed");
+            return SPAI_ERR_DEVICE;
+        }
+        L->host_buf_n = need;
+    }
     return SPAI_OK;
 }
 

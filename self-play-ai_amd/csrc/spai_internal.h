@@ -170,6 +170,13 @@ struct spai_learner {
     spai::DevBuf<float> wpart_side[kWgStreams];
     void *comm = nullptr;            // ncclComm_t (learner.hip)
     int rank = 0, world = 1;
+    // host collective in place of RCCL (spai_learner_set_host_comm): every
+    // all-reduce of the step is staged through `host_buf` (pinned) and summed by
+    // the caller's function
+    spai_host_allreduce host_ar = nullptr;
+    void *host_ar_user = nullptr;
+    float *host_buf = nullptr;
+    size_t host_buf_n = 0;
 };
 
 
@@ -240,6 +247,7 @@ int learner_train_epochs(spai_learner *l, uint32_t n, const float *states, const
                          uint32_t epochs, uint32_t batch, uint64_t seed, float *loss3);
 int learner_set_comm(spai_learner *l, int rank, int world, const uint8_t *id);
 int learner_broadcast(spai_learner *l, int root);
+int learner_set_host_comm(spai_learner *l, int rank, int world, spai_host_allreduce fn, void *user);
 int comm_unique_id(uint8_t *id);
 
 // interop.cpp

@@ -18,6 +18,8 @@ import socket
 import struct
 import time
 
+import numpy as np
+
 
 def _send(sock, obj):
     data = json.dumps(obj).encode()
@@ -32,6 +34,15 @@ def _recv_exact(sock, n):
             raise ConnectionError("host group peer closed the connection")
         buf += chunk
     return bytes(buf)
+
+
+def _send_bytes(sock, data):
+    sock.sendall(struct.pack("<Q", len(data)) + data)
+
+
+def _recv_bytes(sock):
+    (n,) = struct.unpack("<Q", _recv_exact(sock, 8))
+    return _recv_exact(sock, n)
 
 
 def _recv(sock):
@@ -94,6 +105,25 @@ class HostGroup:
 
     def barrier(self):
         self.allgather(0)
+
+    def allreduce_f32(self, buf):
+        """element-wise sum of a float32 array over the ranks, in place, summed in
+        rank order at rank 0 (so every rank gets bit-identical values) — the host
+        collective of spai.Learner.set_host_comm"""
+        if self.world == 1:
+            return buf
+        if self.rank == 0:
+            tot = np.array(buf, np.float32, copy=True)
+            for r in range(1, self.world):
+                tot += np.frombuffer(_recv_bytes(self.peers[r]), np.float32)
+            data = tot.tobytes()
+            for r in range(1, self.world):
+                _send_bytes(self.peers[r], data)
+            buf[:] = tot
+        else:
+            _send_bytes(self.sock, np.ascontiguousarray(buf, np.float32).tobytes())
+            buf[:] = np.frombuffer(_recv_bytes(self.sock), np.float32)
+        return buf
 
     def broadcast_bytes(self, data=None):
         """rank 0's bytes on every rank"""

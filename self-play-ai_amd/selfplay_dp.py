@@ -26,8 +26,9 @@ import spai
 
 class Config3Rank:
     def __init__(self, rank, world, uid, games=4096, sims=800, blocks=6, batch=128, train_steps=20, fraction=0.3,
-                 capacity=None, seed=0, device=0):
+                 capacity=None, seed=0, device=0, group=None):
         self.rank, self.world = rank, world
+        self.group = group   # host group (hostgroup.HostGroup): agrees the step count over ranks
         self.games, self.sims, self.blocks = games, sims, blocks
         self.batch, self.train_steps, self.fraction, self.seed = batch, train_steps, fraction, seed
         self.eng = spai.Engine(num_searches=sims, max_trees=games, eval_kind=spai.EVAL_NET, device=device, seed=seed)
@@ -37,7 +38,8 @@ class Config3Rank:
         self.ring = spai.Replay(capacity or batch * 100)
         self.round_no = 0
         self.net = None
-        self.totals = dict(sims=0.0, games=0.0, positions=0.0, samples_pushed=0.0, samples_trained=0.0)
+        self.totals = dict(sims=0.0, games=0.0, positions=0.0, samples_pushed=0.0, samples_trained=0.0,
+                           steps_trained=0.0, steps_skipped=0.0)
         self.seconds = dict(selfplay=0.0, train=0.0, refresh=0.0)
 
     def run_round(self, collect_games=False):
@@ -60,11 +62,20 @@ class Config3Rank:
         self.totals["samples_pushed"] += k
         t0 = time.perf_counter()
         loss = None
-        for _ in range(self.train_steps):
+        # The reference trainer blocks until a batch is buffered (Condvar::wait_while,
+        # learner_concurrent.rs:94-101); a round-synchronous rank cannot wait for samples
+        # that only the next round produces, so it trains the steps every rank can fill
+        # (the minimum over ranks: each step is a collective) and counts the rest as skipped
+        steps = min(self.train_steps, len(self.ring) // self.batch)
+        if self.group is not None and self.world > 1:
+            steps = int(-self.group.allreduce([-steps], "max")[0])
+        for _ in range(steps):
             s, p, v = self.ring.pop(self.batch)
             loss = self.learner.train_batch(s, p, v)
         self.seconds["train"] += time.perf_counter() - t0
-        self.totals["samples_trained"] += self.train_steps * self.batch
+        self.totals["samples_trained"] += steps * self.batch
+        self.totals["steps_trained"] += steps
+        self.totals["steps_skipped"] += self.train_steps - steps
         t0 = time.perf_counter()
         self.learner.broadcast(0)
         self.params = self.learner.params()

@@ -35,7 +35,8 @@ SYMBOLS = [
     "spai_selfplay_run", "spai_engine_set_timing", "spai_engine_timing", "spai_engine_timing_items",
     "spai_net_phase_cycles", "spai_net_bench", "spai_adam_config_default", "spai_learner_create", "spai_learner_destroy",
     "spai_learner_train_batch", "spai_learner_params", "spai_learner_grads", "spai_learner_activation", "spai_comm_unique_id",
-    "spai_learner_set_comm", "spai_learner_broadcast", "spai_params_save_safetensors", "spai_params_load_safetensors",
+    "spai_learner_set_comm", "spai_learner_broadcast", "spai_learner_set_host_comm", "spai_learner_last_batch",
+    "spai_params_save_safetensors", "spai_params_load_safetensors",
     "spai_replay_create", "spai_replay_destroy", "spai_replay_push", "spai_replay_pop", "spai_replay_size",
     "spai_choose_multiple", "spai_pipeline_config_default", "spai_pipeline_run", "spai_learner_train",
     "spai_policy_normalize", "spai_policy_best_action", "spai_policy_sample",
@@ -83,7 +84,7 @@ class AdamConfig(C.Structure):
 
 
 class PipelineConfig(C.Structure):
-    _fields_ = [("n_selfplay", C.c_uint32), ("selfplay_devices", C.POINTER(C.c_int)), ("learner_device", C.c_int),
+    _fields_ = [("struct_size", C.c_uint32), ("n_selfplay", C.c_uint32), ("selfplay_devices", C.POINTER(C.c_int)), ("learner_device", C.c_int),
                 ("games_per_batch", C.c_uint32), ("num_searches", C.c_uint32), ("c", C.c_float),
                 ("temperature", C.c_float), ("batch_size", C.c_uint32), ("batches_per_iter", C.c_uint32),
                 ("train_iters", C.c_uint32), ("replay_capacity", C.c_uint32), ("sample_fraction", C.c_float),
@@ -108,6 +109,8 @@ class PipelineStats(C.Structure):
                [("last_loss", C.c_double * 3)] + \
                [(k, C.c_double) for k in ("weight_version_published", "weight_version_used_max", "seconds")]
 
+
+HOST_ALLREDUCE = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_float), C.c_size_t)
 
 SINK = C.CFUNCTYPE(None, C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_float), C.POINTER(C.c_float),
                    C.POINTER(C.c_float), C.POINTER(C.c_int32))
@@ -174,6 +177,8 @@ def lib():
         L.spai_comm_unique_id.argtypes = [vp]
         L.spai_learner_set_comm.argtypes = [vp, i32, i32, vp]
         L.spai_learner_broadcast.argtypes = [vp, i32]
+        L.spai_learner_set_host_comm.argtypes = [vp, i32, i32, HOST_ALLREDUCE, vp]
+        L.spai_learner_last_batch.argtypes = [vp, P(u32)]
         L.spai_params_save_safetensors.argtypes = [i32, i32, i32, vp, C.c_size_t, C.c_char_p]
         L.spai_params_load_safetensors.argtypes = [i32, i32, i32, C.c_char_p, vp, C.c_size_t]
         L.spai_replay_create.argtypes = [u32, P(vp)]
@@ -440,7 +445,7 @@ class Learner:
         self.params0 = np.ascontiguousarray(params, np.float32)
         self.n = len(self.params0)
         self.blocks, self.hidden = blocks, hidden
-        self.last_batch = 0
+        self._host_ar = None
         self.h = C.c_void_p()
         _check(lib().spai_learner_create(engine.h, blocks, hidden, _p(self.params0), self.n, C.byref(cfg),
                                          C.byref(self.h)))
@@ -452,7 +457,6 @@ class Learner:
         assert len(x) == len(pi) == len(z)
         loss = np.zeros(3, np.float32)
         _check(lib().spai_learner_train_batch(self.h, len(x), _p(x), _p(pi), _p(z), _p(loss)))
-        self.last_batch = len(x)
         return loss   # total, policy, value
 
     def train(self, states, policies, values, epochs=1, batch=128, seed=0):
@@ -463,6 +467,13 @@ class Learner:
         loss = np.zeros(3, np.float32)
         _check(lib().spai_learner_train(self.h, len(z), _p(x), _p(pi), _p(z), epochs, batch, seed, _p(loss)))
         return loss
+
+    @property
+    def last_batch(self):
+        """the batch size of the latest train step (the C side's, so it follows train() too)"""
+        n = C.c_uint32()
+        _check(lib().spai_learner_last_batch(self.h, C.byref(n)))
+        return n.value
 
     def params(self):
         out = np.zeros(self.n, np.float32)
@@ -475,7 +486,7 @@ class Learner:
         return out
 
     def activation(self, layer):
-        """the last train_batch's post-ReLU activations of conv `layer` (stem, residual
+        """the last train step's post-ReLU activations of conv `layer` (stem, residual
         convs, policy head, value head), [B][co][6][7]"""
         nl = 2 * self.blocks + 3
         co = 32 if layer == nl - 2 else 3 if layer == nl - 1 else self.hidden
@@ -486,9 +497,30 @@ class Learner:
     def set_comm(self, rank, world, uid=None):
         buf = None if uid is None else np.frombuffer(bytes(uid), np.uint8).copy()
         _check(lib().spai_learner_set_comm(self.h, rank, world, None if buf is None else _p(buf)))
+        self._host_ar = None
+
+    def set_host_comm(self, rank, world, allreduce):
+        """host collective in place of RCCL: allreduce(buf) sums the float32 array buf
+        over the ranks in place (same rank order everywhere); None drops it"""
+        if allreduce is None:
+            self._host_ar = None
+            _check(lib().spai_learner_set_host_comm(self.h, 0, 1, HOST_ALLREDUCE(), None))
+            return
+
+        def fn(_user, ptr, n):
+            try:
+                allreduce(np.ctypeslib.as_array(ptr, shape=(n,)))
+                return 0
+            except Exception:   # an error must not unwind through C; the step reports it
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        self._host_ar = HOST_ALLREDUCE(fn)   # kept alive while the learner may call it
+        _check(lib().spai_learner_set_host_comm(self.h, rank, world, self._host_ar, None))
 
     def broadcast(self, root=0):
-        """RCCL broadcast of rank `root`'s parameters to every rank (weight refresh)"""
+        """RCCL (or host-collective) broadcast of rank `root`'s parameters to every rank"""
         _check(lib().spai_learner_broadcast(self.h, root))
 
     def close(self):
@@ -580,6 +612,7 @@ def pipeline_run(init_params, selfplay_devices=(0,), learner_device=0, checkpoin
     events: a list that receives every ring event in ring order as a dict (kind,
     worker, batch, version, n, positions, ring_size, and copies of the samples)"""
     cfg = PipelineConfig()
+    cfg.struct_size = C.sizeof(PipelineConfig)
     _check(lib().spai_pipeline_config_default(C.byref(cfg)))
     devs = (C.c_int * len(selfplay_devices))(*selfplay_devices)
     cfg.n_selfplay = len(selfplay_devices)

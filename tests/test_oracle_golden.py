@@ -249,6 +249,34 @@ def test_learner_oracle_vs_torch_golden(oracle):
     check_learner_params(P3, z["params3"], [g_ref], blocks, hidden, 3, tol=1e-4)
 
 
+def test_learner_oracle_dp_restatement(oracle):
+    """the float64 DDP restatement (train_step_dp) that pins the world > 1 learner:
+    one rank is train_step; two ranks holding the same batch are train_step on it
+    (weights 1/2 + 1/2, running statistics the mean of equal values); unequal
+    batches weight each rank's mean gradient by B_r / sum B"""
+    import learner_ref as LR
+    z = np.load(os.path.join(GOLDEN, "learner_c4_1x64.npz"))
+    blocks, hidden, seed, B, K = [int(v) for v in z["meta"]]
+    p0 = oracle.init_params(oracle.GAME_CONNECT4, blocks, hidden, seed)
+    n = len(p0)
+    b = (z["states"][0], z["policies"][0], z["values"][0])
+    P1, m1, v1, l1, g1 = LR.train_step(p0, np.zeros(n), np.zeros(n), 0, *b, blocks, hidden)
+    Pd, md, vd, ld, gd, _ = LR.train_step_dp(p0, np.zeros(n), np.zeros(n), 0, [b], blocks, hidden)
+    np.testing.assert_array_equal(Pd, P1)
+    np.testing.assert_array_equal(gd, g1)
+    Pd, _, _, ld, gd, _ = LR.train_step_dp(p0, np.zeros(n), np.zeros(n), 0, [b, b], blocks, hidden)
+    np.testing.assert_allclose(Pd, P1, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(gd, g1, rtol=0, atol=1e-12 * np.abs(g1).max())
+    s_ = np.concatenate(list(z["states"]))
+    p_ = np.concatenate(list(z["policies"]))
+    v_ = np.concatenate(list(z["values"]))
+    ra, rb = (s_[:12], p_[:12], v_[:12]), (s_[12:32], p_[12:32], v_[12:32])
+    _, _, _, _, gd, parts = LR.train_step_dp(p0, np.zeros(n), np.zeros(n), 0, [ra, rb], blocks, hidden)
+    _, ga, _ = LR.forward_backward(p0, *ra, blocks, hidden)
+    _, gb, _ = LR.forward_backward(p0, *rb, blocks, hidden)
+    np.testing.assert_allclose(gd, (12 * ga + 20 * gb) / 32, rtol=0, atol=1e-12 * np.abs(gd).max())
+
+
 @pytest.mark.parametrize("fixture,k", [("mcts_f32net.npz", 6), ("mcts_f32net_6x64.npz", 1)])
 def test_mcts_f32net_fixture(oracle, fixture, k):
     """tests/golden/mcts_f32net*.npz (search with the fp32 net, gen_f32net_golden.py)

@@ -51,6 +51,16 @@ WORKER = textwrap.dedent("""
     parts = g.allgather((res["game"].tolist(), res["value"].tolist()))
     uid = g.broadcast_bytes(bytes(range(128)) if r == 0 else None)   # the RCCL unique-id hand-off
     assert uid == bytes(range(128))
+    # the learner's host collective (spai.Learner.set_host_comm): float32 sum in rank order
+    a = (np.arange(1000, dtype=np.float32) * np.float32(0.1 * (r + 1))).astype(np.float32)
+    b = a.copy()
+    g.allreduce_f32(b)
+    exp = np.arange(1000, dtype=np.float32) * np.float32(0.1)
+    exp = exp + (np.arange(1000, dtype=np.float32) * np.float32(0.2)).astype(np.float32)
+    assert np.array_equal(b, exp.astype(np.float32)), "allreduce_f32"
+    neg0 = np.full(4, -0.0, np.float32) if r else np.array([0.0, -0.0, 1.5, -2.0], np.float32)
+    g.allreduce_f32(neg0)   # the host broadcast: root's values + -0.0 keeps every bit, signed zeros too
+    assert np.array_equal(neg0.view(np.uint32), np.array([0.0, -0.0, 1.5, -2.0], np.float32).view(np.uint32))
     if r == 0:
         print(json.dumps({{"sims": sims, "tmax": tmax, "parts": parts}}))
     g.close()
