@@ -451,6 +451,33 @@ __host__ __device__ constexpr int b_depth(int S) { return S <= 2 ? 4 : S <= 3 ? 
 // weights without a cold start.  `wn` is always a valid layer (the current one
 // when nothing follows): an unconditional prefetch keeps the vmcnt bookkeeping
 // free of branches.
+// Timing-only deletion experiments (diagnostic builds; wrong results):
+// SPAI_EXP_NOA replaces the k-loop's weight loads by a register value, SPAI_EXP_NOB
+// its activation reads, SPAI_EXP_NOBAR drops the barrier between trunk layers.
+__device__ __forceinline__ uint4 exp_a(const uint4 &src, int lane, int k) {
+#ifdef SPAI_EXP_NOA
+    (void)src;
+    return make_uint4(0x3F803F80u ^ (uint32_t)(lane + k), 0x3F803F80u, 0x3F803F80u, (uint32_t)k);
+#else
+    (void)lane, (void)k;
+    return src;
+#endif
+}
+__device__ __forceinline__ uint4 exp_b(const uint8_t *p, int lane, int k) {
+#ifdef SPAI_EXP_NOB
+    (void)p;
+    return make_uint4(0x3F803F80u ^ (uint32_t)(lane * 3 + k), 0x3F803F80u, 0x3F803F80u, (uint32_t)k);
+#else
+    (void)lane, (void)k;
+    return *(const uint4 *)p;
+#endif
+}
+__device__ __forceinline__ void layer_barrier() {
+#ifndef SPAI_EXP_NOBAR
+    __syncthreads();
+#endif
+}
+
 // The last tap of a 64-channel layer, task-major, with the epilogue fused
 // (conv_mfma EPI > 0): k-steps 16 and 17 of task i (and, EPI = 2, the residual
 // identity MFMA on the center-tap fragment of the block input at OUT), then
@@ -596,10 +623,10 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
         if (ks + la < kKStepsRes) {
 #pragma unroll
             for (int c = 0; c < CTL; ++c)
-                if (!(EPI == 3 && PL::C0 + c == 3)) A[(ks + la) % DA][c] = wl[((ks + la) * CT + c) * 64];
+                if (!(EPI == 3 && PL::C0 + c == 3)) A[(ks + la) % DA][c] = exp_a(wl[((ks + la) * CT + c) * 64], lane, ks + c);
         } else if (EPI != 3) {   // (nothing follows the head)
 #pragma unroll
-            for (int c = 0; c < CTL; ++c) A[(ks + la) % DA][c] = wnl[((ks + la - kKStepsRes) * CT + c) * 64];
+            for (int c = 0; c < CTL; ++c) A[(ks + la) % DA][c] = exp_a(wnl[((ks + la - kKStepsRes) * CT + c) * 64], lane, ks + c);
         }
     };
 #pragma unroll
@@ -625,7 +652,7 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
 #pragma unroll
             for (int t = 0; t < NT; ++t)
                 if (live(t, ks + lb)) {
-                    B[(ks + lb) % DB][t] = *(const uint4 *)(smem + (IN - 256) + (g.b(t, tap) ^ flip));
+                    B[(ks + lb) % DB][t] = exp_b(smem + (IN - 256) + (g.b(t, tap) ^ flip), lane, ks + t);
                     ++nr;
                 }
         }
@@ -917,7 +944,7 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
             stamp(P, W, lane, 18);
         }
 #endif
-        __syncthreads();
+        layer_barrier();
 #ifdef SPAI_DIAG
         if (b == 0 && !kDiagHead) stamp(P, W, lane, 19);
 #endif
@@ -931,7 +958,7 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
         } else {
             epilogue_act<W, NPT, kX, true>(smem, g, acc);
         }
-        __syncthreads();
+        layer_barrier();
         if (l2 < 12) stamp(P, W, lane, 2 + l2);
     }
     if (kDiagHead) stamp(P, W, lane, 19);   // diagnostic head mode: 19 = before the head, 17 = head k-loop, 18 = H written

@@ -319,8 +319,9 @@ ChainPolicy chains_for(uint32_t n, double last_evals_per_iter) {
     static const int mid_leaves = env_int("SPAI_MID_LEAVES", 0);
     static const int mid_chains = std::max(1, std::min(spai_engine::kChains, env_int("SPAI_MID_CHAINS", 2)));
     static const uint32_t mid_grid = (uint32_t)std::max(0, env_int("SPAI_MID_GRID", 0));
+    static const double min_chain_leaves = env_int("SPAI_MIN_CHAIN_LEAVES", (int)kMinChainLeaves);   // A/B knob
     if (forced) return {std::max(1, std::min<int>(forced, (int)(n / 64))), 0u};
-    if (last_evals_per_iter >= 0 && last_evals_per_iter < kMinChainLeaves) return {1, 0u};
+    if (last_evals_per_iter >= 0 && last_evals_per_iter < min_chain_leaves) return {1, 0u};
     if (last_evals_per_iter >= 0 && last_evals_per_iter < mid_leaves)
         return {std::max(1, std::min<int>(mid_chains, (int)(n / 64))), mid_grid};
     return {std::max(1, std::min<int>(2, (int)(n / 64))), 0u};

@@ -175,7 +175,8 @@ def test_f32_and_bf16_nets_agree_on_search(spai, fixture):
         e.close()
     (pa, _, va, na), (pb, _, vb, nb) = out
     np.testing.assert_array_equal(na, nb)
-    assert np.abs(pa - pb).max() < 0.25
+    # the fixture's few roots at its sim count; the stated tolerance is the
+    # distribution-level one of test_bf16_search_statistics (512 roots, 800 sims)
     assert np.mean(np.abs(pa - pb).sum(1)) < 0.15
 
 
@@ -197,11 +198,13 @@ def test_bf16_search_statistics(spai, oracle):
     above) on 512 roots at the bench's 800 sims and the bench's 6x64 net: the
     stated tolerance of the throughput path's root policy (the move-sampling and
     training target), over the distribution of roots rather than one max entry.
-    Bounds (measured 2026-10 on MI355X, set at ~2x the observed values):
-      mean |dpi| per legal entry <= 0.01, its 99th percentile <= 0.06,
-      mean L1 per root <= 0.05, 99th percentile <= 0.25,
-      most-visited child the same (fp32 ties counted) on >= 90 % of roots;
-    priors within 2e-2 and values within 3e-2 of fp32 at every root.
+    Bounds, set at 2.5-4x the values measured on MI355X (profiles/r04/bf16_search_stats.json:
+    entry mean 8.2e-4, p99 7.5e-3; L1 mean 5.7e-3, p99 4.7e-2; top child 99.4 %;
+    priors 2.2e-3, values 2.4e-3):
+      mean |dpi| per legal entry <= 2.5e-3, its 99th percentile <= 2.5e-2,
+      mean L1 per root <= 2e-2, 99th percentile <= 0.15,
+      most-visited child the same (fp32 ties counted) on >= 97 % of roots;
+    priors and values within 1e-2 of fp32 at every root.
     SPAI_STATS_OUT=<path> writes the measured statistics as JSON."""
     import json
     z = _golden("mcts_f32net_6x64.npz")
@@ -232,7 +235,7 @@ def test_bf16_search_statistics(spai, oracle):
     if os.environ.get("SPAI_STATS_OUT"):
         with open(os.environ["SPAI_STATS_OUT"], "w") as f:
             json.dump(st, f, indent=1)
-    assert st["prior_abs_max"] <= 2e-2 and st["value_abs_max"] <= 3e-2, st
-    assert st["entry_abs_mean"] <= 0.01 and st["entry_abs_p99"] <= 0.06, st
-    assert st["root_l1_mean"] <= 0.05 and st["root_l1_p99"] <= 0.25, st
-    assert st["top_child_agree_ties"] >= 0.90, st
+    assert st["prior_abs_max"] <= 1e-2 and st["value_abs_max"] <= 1e-2, st
+    assert st["entry_abs_mean"] <= 2.5e-3 and st["entry_abs_p99"] <= 2.5e-2, st
+    assert st["root_l1_mean"] <= 2e-2 and st["root_l1_p99"] <= 0.15, st
+    assert st["top_child_agree_ties"] >= 0.97, st
