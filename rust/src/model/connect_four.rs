@@ -54,6 +54,29 @@ impl Drop for Gpu {
     }
 }
 
+/// the device learner for this Net (engine + spai_learner), created on the first
+/// train step from the VarStore's values; its Adam moments persist across steps
+/// like the trainer's tch optimizer (learner_concurrent.rs:42-48)
+struct Trainer {
+    engine: *mut sys::spai_engine,
+    learner: *mut sys::spai_learner,
+    n_params: usize,
+}
+unsafe impl Send for Trainer {}
+
+impl Drop for Trainer {
+    fn drop(&mut self) {
+        unsafe {
+            if !self.learner.is_null() {
+                sys::spai_learner_destroy(self.learner);
+            }
+            if !self.engine.is_null() {
+                sys::spai_engine_destroy(self.engine);
+            }
+        }
+    }
+}
+
 pub struct Net {
     torso: SequentialT,
     policy_head: SequentialT,
@@ -61,6 +84,7 @@ pub struct Net {
     blocks: u32,
     vars: Vec<Tensor>,   // construction (= spai_net_create flat) order
     dev: Mutex<Option<Gpu>>,
+    trainer: Mutex<Option<Trainer>>,
 }
 
 fn conv_bn(vs: &nn::Path, ci: i64, co: i64, vars: &mut Vec<Tensor>) -> (nn::Conv2D, nn::BatchNorm) {
@@ -106,7 +130,7 @@ impl super::Net for Net {
         let value_head = nn::seq_t().add(vc).add(vb).add_fn(|x| x.relu()).add_fn(|x| x.flat_view()).add(vl)
             .add_fn(|x| x.tanh());
         assert_eq!(h, 64, "the device net is built for 64 hidden channels");
-        Self { torso, policy_head, value_head, blocks, vars, dev: Mutex::new(None) }
+        Self { torso, policy_head, value_head, blocks, vars, dev: Mutex::new(None), trainer: Mutex::new(None) }
     }
 
     // train = true: the tch graph (the trainer's autograd path, model/mod.rs:100-149);
@@ -130,6 +154,56 @@ impl super::Net for Net {
     fn search_trees(&self, args: &MctsArgs, trees: &mut [&mut Tree<C4State>])
         -> Vec<super::SearchResult<C4State>> {
         self.device_search(args, trees)
+    }
+
+    fn device_train_batch(&self, states: &Tensor, policies: &Tensor, values: &Tensor) -> Option<f64> {
+        Some(self.device_train(states, policies, values))
+    }
+}
+
+impl Net {
+    /// one device train step (spai_learner_train_batch, fp32 on the exact-f32 MFMA),
+    /// then the VarStore variables (and through them the trainer's checkpoints and
+    /// the self-play weight copy, learner_concurrent.rs:155-161) take the new values
+    fn device_train(&self, states: &Tensor, policies: &Tensor, values: &Tensor) -> f64 {
+        let flat = |t: &Tensor| Vec::<f32>::try_from(t.to_device(Device::Cpu).to_kind(Kind::Float).contiguous().view(-1)).unwrap();
+        let (x, pi, z) = (flat(states), flat(policies), flat(values));
+        let n = z.len();
+        assert!(x.len() == n * 126 && pi.len() == n * 7, "train batch shapes: [n][3][6][7], [n][7], [n](x1)");
+        let mut g = self.trainer.lock().unwrap();
+        if g.is_none() {
+            let mut cfg = sys::spai_config::default();
+            sys::check(unsafe { sys::spai_config_default(sys::SPAI_GAME_CONNECT4, &mut cfg) });
+            cfg.max_trees = 1;
+            cfg.num_searches = 1;
+            let device = std::env::var("SPAI_TRAIN_DEVICE").or_else(|_| std::env::var("SPAI_DEVICE")).ok()
+                .and_then(|v| v.parse().ok()).unwrap_or(0);
+            let mut e = std::ptr::null_mut();
+            sys::check(unsafe { sys::spai_engine_create(sys::SPAI_GAME_CONNECT4, &cfg, device, &mut e) });
+            let p = self.params();
+            let mut l = std::ptr::null_mut();
+            sys::check(unsafe {
+                sys::spai_learner_create(e, self.blocks as i32, 64, p.as_ptr(), p.len(), std::ptr::null(), &mut l)
+            });
+            *g = Some(Trainer { engine: e, learner: l, n_params: p.len() });
+        }
+        let t = g.as_mut().unwrap();
+        let mut loss = [0f32; 3];
+        sys::check(unsafe {
+            sys::spai_learner_train_batch(t.learner, n as u32, x.as_ptr(), pi.as_ptr(), z.as_ptr(), loss.as_mut_ptr())
+        });
+        let mut p = vec![0f32; t.n_params];
+        sys::check(unsafe { sys::spai_learner_params(t.learner, p.as_mut_ptr(), p.len()) });
+        let _guard = tch::no_grad_guard();
+        let mut off = 0usize;
+        for v in &self.vars {
+            let k = v.numel();
+            let src = Tensor::from_slice(&p[off..off + k]).view(v.size().as_slice()).to_device(v.device());
+            v.shallow_clone().copy_(&src);
+            off += k;
+        }
+        assert_eq!(off, p.len(), "VarStore variables vs the device learner's flat parameters");
+        loss[0] as f64
     }
 }
 

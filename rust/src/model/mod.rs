@@ -52,6 +52,17 @@ pub trait Net {
         panic!("{}: this Net has no device search (libspai implements Connect4, TicTacToe and chess)",
                std::any::type_name::<Self>())
     }
+
+    /// ModelTrainerWorker::train_batch (learner_concurrent.rs:72-85) on the device:
+    /// one train-mode forward, the policy NLL + value MSE loss, backward and one
+    /// Adam step (spai_learner_train_batch), with this net's VarStore variables
+    /// overwritten by the updated parameters; returns the total loss.  None: this
+    /// net has no device learner and the caller keeps its tch step
+    /// (patches/device_trainer.patch makes train_batch try this first).
+    fn device_train_batch(&self, states: &Tensor, policies: &Tensor, values: &Tensor) -> Option<f64> {
+        let _ = (states, policies, values);
+        None
+    }
 }
 
 pub struct Model<T: Net> {

@@ -198,6 +198,10 @@ extern "C" {
     pub fn spai_comm_unique_id(id: *mut u8) -> c_int;
     pub fn spai_learner_set_comm(l: *mut spai_learner, rank: c_int, world: c_int, id: *const u8) -> c_int;
     pub fn spai_learner_broadcast(l: *mut spai_learner, root: c_int) -> c_int;
+    pub fn spai_learner_set_host_comm(l: *mut spai_learner, rank: c_int, world: c_int,
+                                      f: Option<extern "C" fn(*mut c_void, *mut f32, usize) -> c_int>,
+                                      user: *mut c_void) -> c_int;
+    pub fn spai_learner_last_batch(l: *mut spai_learner, n: *mut u32) -> c_int;
 
     // checkpoints (VarStore::save / load: learner.rs:192, main.rs:61)
     pub fn spai_params_save_safetensors(game: c_int, blocks: c_int, hidden: c_int, params: *const f32, n: usize,

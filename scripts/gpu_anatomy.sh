@@ -12,6 +12,6 @@ run() {   # $1 = label, rest = env assignments
   env "$@" SPAI_TRACE_MOVES=$PWD/$O/moves_$L.csv timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d /tmp/an_$L -o an -- \
     python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-isolated --no-rules-bench --no-chess > $O/bench_$L.json 2> $O/bench_$L.err || { tail -5 $O/bench_$L.err; return 1; }
   f=$(find /tmp/an_$L -name '*kernel_trace.csv' | head -1)
-  python3 scripts/step_anatomy.py "$f" $O/anatomy_$L.json > $O/anatomy_$L.txt && tail -48 $O/anatomy_$L.txt
+  python3 scripts/step_anatomy.py "$f" $O/anatomy_$L.json ${DUMP_MOVES:-2,12,25,33,39} $O/timeline_$L.csv > $O/anatomy_$L.txt && tail -48 $O/anatomy_$L.txt
 }
 run base && for ab in ${ENV_AB:-}; do run $(echo $ab | tr '=,' '__') $(echo $ab | tr ',' ' ') || exit 1; done

@@ -3,7 +3,9 @@ cut into moves at each k_root_stats (one per search call), and per move the
 script reports the wall time, the forward (k_forward) launches with their mean
 duration, the tree-kernel launches (k_select / k_expand_select / k_expand) with
 theirs, and how the wall splits into time with 0, 1 or 2 forwards running.
-usage: step_anatomy.py kernel_trace.csv [out.json]"""
+usage: step_anatomy.py kernel_trace.csv [out.json] [moves_to_dump out.csv]
+(moves_to_dump: comma-separated move numbers; their first 120 kernels are written
+with stream, start and end in microseconds from the move's first kernel)"""
 import collections
 import csv
 import json
@@ -18,7 +20,9 @@ def kname(s):
 
 def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
-    ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kname(r["Kernel_Name"])) for r in rows)
+    skey = "Stream_Id" if "Stream_Id" in rows[0] else ("Queue_Id" if "Queue_Id" in rows[0] else None)
+    ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), kname(r["Kernel_Name"]),
+                 r.get(skey, "0") if skey else "0") for r in rows)
     moves, cur = [], []
     for k in ks:
         cur.append(k)
@@ -29,11 +33,11 @@ def main():
     for i, mv in enumerate(moves):
         t0, t1 = mv[0][0], mv[-1][1]
         by = collections.defaultdict(list)
-        for s, e, n in mv:
+        for s, e, n, _ in mv:
             by[n].append((e - s) / 1e3)
         # time with 0/1/2+ forwards running (sweep over forward intervals)
         ev = []
-        for s, e, n in mv:
+        for s, e, n, _ in mv:
             if n == "k_forward":
                 ev += [(s, 1), (e, -1)]
         ev.sort()
@@ -67,6 +71,14 @@ def main():
           tuple(agg[k] / tot for k in ("no_fwd_frac", "one_fwd_frac", "two_fwd_frac")))
     if len(sys.argv) > 2:
         json.dump(out, open(sys.argv[2], "w"), indent=0)
+    if len(sys.argv) > 4:
+        with open(sys.argv[4], "w") as f:
+            f.write("move,kernel,stream,start_us,end_us\n")
+            for m in (int(v) for v in sys.argv[3].split(",")):
+                if m < len(moves):
+                    t0 = moves[m][0][0]
+                    for s, e, n, q in moves[m][:120]:
+                        f.write("%d,%s,%s,%.2f,%.2f\n" % (m, n, q, (s - t0) / 1e3, (e - t0) / 1e3))
 
 
 if __name__ == "__main__":

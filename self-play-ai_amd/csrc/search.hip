@@ -52,6 +52,7 @@ struct TreeView {
     uint32_t *path;
     uint8_t *depth;
     uint32_t *slot;   // the tree's leaf slot in the current batch, kNoSlot if terminal
+    uint32_t *left;   // tail run-on mode: search iterations the tree still has to run
 };
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
@@ -88,16 +89,20 @@ __device__ __forceinline__ void backup(uint4 *nodes, const uint32_t *path, int d
     for (int lvl = lane8; lvl <= d; lvl += kLanesPerTree) backup_level(nodes, path[lvl], d, lvl, v);
 }
 
-// PUCT descent of tree t (mcts.rs:235-250) by its 8 lanes; a live leaf gets a
-// slot in batch B (recorded in T.slot[t]), a terminal leaf is backed up in place
-__device__ __forceinline__ void select_tree(const TreeView &T, const BatchView &B, uint32_t t, int lane8, float c,
-                                            uint32_t *err) {
-    if (lane8 == 0) T.slot[t] = kNoSlot;
+// One PUCT descent of tree t (mcts.rs:235-250) by its 8 lanes.  A terminal leaf
+// is backed up in place (mcts.rs:245-247) and kTerminal returned; a live leaf is
+// returned as kLive with its position in (x, o, n) and its path recorded (T.path,
+// T.depth); kError after a NaN UCB or an over-deep path (flag set in err).
+enum Descent { kTerminal = 0, kLive = 1, kError = 2 };
+__device__ __forceinline__ Descent descend(const TreeView &T, uint32_t t, int lane8, float c, uint32_t *err,
+                                           uint64_t &x, uint64_t &o, uint8_t &n) {
     uint4 *nodes = T.nodes + (size_t)t * T.cap;
     uint32_t *path = T.path + (size_t)t * kMaxDepth;
     uint32_t node = T.root[t];
-    uint64_t x = T.root_x[t], o = T.root_o[t];
-    uint8_t n = T.root_n[t], status = T.root_status[t];
+    x = T.root_x[t];
+    o = T.root_o[t];
+    n = T.root_n[t];
+    uint8_t status = T.root_status[t];
     uint4 rec = nodes[node];
     // path levels == lane8 (mod 8) kept in this lane's registers (kMaxDepth = 6 x 8)
     uint32_t p0 = node, p1 = 0, p2 = 0, p3 = 0, p4 = 0, p5 = 0;
@@ -116,7 +121,7 @@ __device__ __forceinline__ void select_tree(const TreeView &T, const BatchView &
         // before the argmax, so lanes never split onto different children
         if ((__ballot(u != u) >> (threadIdx.x & 63 & ~(kLanesPerTree - 1))) & 0xFFull) {
             if (lane8 == 0) atomicOr(err, kErrNan);
-            return;
+            return kError;
         }
         // argmax with ties to the LAST child (Iterator::max_by, mcts.rs:110-113)
         float bu = u;
@@ -146,7 +151,7 @@ __device__ __forceinline__ void select_tree(const TreeView &T, const BatchView &
         ++d;
         if (d >= kMaxDepth) {
             if (lane8 == 0) atomicOr(err, kErrDepth);
-            return;
+            return kError;
         }
         if ((d & 7) == lane8) {
             path[d] = node;
@@ -169,9 +174,14 @@ __device__ __forceinline__ void select_tree(const TreeView &T, const BatchView &
             const int lvl = lane8 + 8 * j;
             if (lvl <= d) backup_level(nodes, pr[j], d, lvl, v);
         }
-        return;
+        return kTerminal;
     }
-    // live leaf -> batch slot (mcts.rs:249-250)
+    return kLive;
+}
+
+// live leaf -> batch slot (mcts.rs:249-250)
+__device__ __forceinline__ void slot_leaf(const TreeView &T, const BatchView &B, uint32_t t, int lane8, uint64_t x,
+                                          uint64_t o, uint8_t n) {
     if (lane8 == 0) {
         const uint32_t slot = atomicAdd(B.count, 1u);
         const bool xm = c4::x_to_move(n);
@@ -180,6 +190,39 @@ __device__ __forceinline__ void select_tree(const TreeView &T, const BatchView &
         B.mine[slot] = xm ? x : o;
         B.theirs[slot] = xm ? o : x;
     }
+}
+
+// One search iteration's selection for tree t: a live leaf gets a slot in batch
+// B (recorded in T.slot[t]), a terminal leaf is backed up in place.
+//
+// RUN_ON (tail mode, search()): the tree runs its remaining iterations (T.left)
+// in this launch for as long as they end on terminal leaves -- each is backed
+// up, then the next descent starts -- and stops at the first live leaf, which
+// goes to the batch.  The tree's iterations keep the reference's order (select,
+// backprop, select, ...), so the results equal one descent per launch; a launch
+// then lasts as long as its longest terminal run, which pays off only late in a
+// game, where most iterations need no evaluation.
+template <bool RUN_ON>
+__device__ __forceinline__ void select_tree(const TreeView &T, const BatchView &B, uint32_t t, int lane8, float c,
+                                            uint32_t *err) {
+    if (lane8 == 0) T.slot[t] = kNoSlot;
+    uint64_t x, o;
+    uint8_t n;
+    if (!RUN_ON) {
+        if (descend(T, t, lane8, c, err, x, o, n) == kLive) slot_leaf(T, B, t, lane8, x, o, n);
+        return;
+    }
+    uint32_t left = T.left[t];
+    while (left > 0) {
+        --left;
+        const Descent r = descend(T, t, lane8, c, err, x, o, n);
+        if (r == kLive) slot_leaf(T, B, t, lane8, x, o, n);
+        if (r != kTerminal) break;
+        // the next descent reads records the other lanes of this tree just backed
+        // up: same wave, made visible as in k_expand_select
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    }
+    if (lane8 == 0) T.left[t] = left;
 }
 
 // expand leaf slot s of batch B (mcts.rs:116-143) and back its value up (:145-159)
@@ -211,6 +254,7 @@ __device__ __forceinline__ void expand_leaf(const TreeView &T, const BatchView &
     backup(nodes, path, d, B.value[s], lane8);
 }
 
+template <bool RUN_ON>
 __global__ __launch_bounds__(kBlock) void k_select(TreeView T, BatchView B, const uint32_t *__restrict__ active,
                                                    uint32_t n_active, float c, uint32_t *err) {
     const uint32_t gi = (blockIdx.x * blockDim.x + threadIdx.x) / kLanesPerTree;
@@ -218,13 +262,14 @@ __global__ __launch_bounds__(kBlock) void k_select(TreeView T, BatchView B, cons
     __builtin_amdgcn_s_setprio(SPAI_TREE_PRIO);   // experiment: issue priority against the co-resident forward
 #endif
     if (gi >= n_active) return;
-    select_tree(T, B, active[gi], threadIdx.x & (kLanesPerTree - 1), c, err);
+    select_tree<RUN_ON>(T, B, active[gi], threadIdx.x & (kLanesPerTree - 1), c, err);
 }
 
 // expand this iteration's leaf of every tree (batch `cur`), then select the next
 // iteration's leaf into batch `nxt`.  A tree's lanes are one group of 8 in one
 // wave: its expand stores are made visible to its own select loads by a
 // workgroup-scope fence (vmcnt(0); the CU's L1 is coherent within a workgroup).
+template <bool RUN_ON>
 __global__ __launch_bounds__(kBlock) void k_expand_select(TreeView T, BatchView cur, BatchView nxt,
                                                           const uint32_t *__restrict__ active, uint32_t n_active,
                                                           float c, uint32_t *err) {
@@ -238,7 +283,13 @@ __global__ __launch_bounds__(kBlock) void k_expand_select(TreeView T, BatchView 
     const uint32_t s = T.slot[t];
     if (s != kNoSlot) expand_leaf(T, cur, s, lane8, err);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    select_tree(T, nxt, t, lane8, c, err);
+    select_tree<RUN_ON>(T, nxt, t, lane8, c, err);
+}
+
+// tail mode: every active tree has all `iters` iterations of this search call ahead
+__global__ void k_set_left(TreeView T, const uint32_t *__restrict__ active, uint32_t n, uint32_t iters) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) T.left[active[i]] = iters;
 }
 
 __global__ __launch_bounds__(kBlock) void k_eval_stub(BatchView B, uint32_t max_n, int kind) {
@@ -283,7 +334,7 @@ __global__ void k_trees_init(TreeView T, uint32_t first_tree, uint32_t n) {
 TreeView tree_view(spai_engine *e) {
     Trees &T = e->trees;
     return TreeView{T.nodes.p, T.cap, T.root.p, T.next_free.p, T.root_x.p, T.root_o.p, T.root_n.p, T.root_status.p,
-                    T.path.p, T.depth.p, T.slot.p};
+                    T.path.p, T.depth.p, T.slot.p, T.left.p};
 }
 
 // chain `chain`'s leaf batch of search iteration `it`: buffers by parity, counter per iteration
@@ -301,6 +352,10 @@ BatchView batch_view(spai_engine *e, int chain, uint32_t it) {
 // kMinChainLeaves leaves per iteration.  (SPAI_CHAINS=k forces up to k chains,
 // for A/B measurements.)  The split never changes results: trees are independent.
 constexpr double kMinChainLeaves = 64;
+// tail mode (select_tree RUN_ON) below this many leaves per iteration in the
+// previous search call; host checks for the end every kTailChunk passes
+constexpr double kTailLeaves = 64;
+constexpr uint32_t kTailChunk = 4;
 static int env_int(const char *name, int dflt) {
     const char *v = std::getenv(name);
     return v ? std::atoi(v) : dflt;
@@ -414,6 +469,7 @@ int trees_create(spai_engine *e, uint32_t n) {
         SPAI_TRY(T.path.alloc((size_t)n * kMaxDepth));
         SPAI_TRY(T.depth.alloc(n));
         SPAI_TRY(T.slot.alloc(n));
+        SPAI_TRY(T.left.alloc(n));
         SPAI_TRY(e->active.alloc(n));
         SPAI_TRY(e->stats.alloc((size_t)n * 8));
         for (Batch &B : e->batch) {   // one double-buffered leaf batch per search chain
@@ -473,11 +529,18 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
         off[h] = (uint32_t)((uint64_t)n * h / nchain);
         cnt[h] = (uint32_t)((uint64_t)n * (h + 1) / nchain) - off[h];
     }
+    // tail mode (select_tree RUN_ON): late in a game, when the previous search call
+    // of these trees evaluated fewer than SPAI_TAIL_LEAVES leaves per iteration
+    // (a single chain then); 0 turns it off
+    static const double tail_leaves = env_int("SPAI_TAIL_LEAVES", (int)kTailLeaves);
+    const bool tail = nchain == 1 && num_searches > 0 && e->last_evals_per_iter >= 0 &&
+                      e->last_evals_per_iter < tail_leaves;
     for (int h = 0; h < nchain; ++h) {   // per-iteration leaf counters (also the batch slot counters)
         Batch &B = e->batch[h];
         // at least one counter even for num_searches == 0, so the memset never sees a
-        // null buffer on a fresh engine
-        const uint32_t nc = std::max<uint32_t>(num_searches, 1);
+        // null buffer on a fresh engine; tail mode runs up to num_searches + 1 passes
+        // in chunks of kTailChunk
+        const uint32_t nc = std::max<uint32_t>(num_searches, 1) + (tail ? kTailChunk + 1 : 0);
         if (B.iter_counts.n < nc) SPAI_TRY(B.iter_counts.alloc(nc));
         SPAI_HIP(hipMemsetAsync(B.iter_counts.p, 0, (size_t)nc * 4, st));
     }
@@ -488,11 +551,44 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
         for (int h = 1; h < nchain; ++h) SPAI_HIP(hipStreamWaitEvent(e->chain_stream[h], e->ev_fork, 0));
     }
     const TreeView tv = tree_view(e);
-    const bool timed = e->timer.enabled;   // samples every chain's launches every stride-th iteration
+    const bool timed = e->timer.enabled && !tail;   // samples every chain's launches every stride-th iteration
+    uint32_t n_counts = num_searches;   // leaf counters to read back per chain
+    if (tail) {
+        // passes on the engine stream: select(0), then per pass p: evaluate(p),
+        // expand(p) + select(p + 1), each select running its trees on through
+        // terminal leaves.  A pass whose select slots no leaf leaves no tree with
+        // iterations to run (a tree stops a launch only at a live leaf), so the
+        // host checks every kTailChunk passes and stops there.
+        const uint32_t g8 = (n + kTreesPerBlock - 1) / kTreesPerBlock;
+        const uint32_t *act = e->active.p;
+        k_set_left<<<(n + 255) / 256, 256, 0, st>>>(tv, act, n, num_searches);
+        k_select<true><<<g8, kBlock, 0, st>>>(tv, batch_view(e, 0, 0), act, n, e->cfg.c, e->err.p);
+        uint32_t p = 0, next = 1;
+        for (;;) {
+            for (uint32_t q = 0; q < kTailChunk; ++q, ++p) {
+                const BatchView bv = batch_view(e, 0, p);
+                if (kind == SPAI_EVAL_NET) {
+                    SPAI_TRY(net_eval_batch(e->net, st, bv.count, n, bv.mine, bv.theirs, bv.priors, bv.value, 0));
+                } else {
+                    k_eval_stub<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(bv, n, kind);
+                }
+                k_expand_select<true><<<g8, kBlock, 0, st>>>(tv, bv, batch_view(e, 0, p + 1), act, n, e->cfg.c,
+                                                             e->err.p);
+            }
+            SPAI_HIP(hipGetLastError());
+            SPAI_HIP(hipMemcpyAsync(&next, e->batch[0].iter_counts.p + p, 4, hipMemcpyDeviceToHost, st));
+            SPAI_HIP(hipStreamSynchronize(st));
+            if (next == 0) break;   // pass p has nothing to evaluate: every tree is done
+            SPAI_CHECK(p <= num_searches + 1, SPAI_ERR_INVALID, "internal: tail passes exceed the iterations");
+            // this chunk's counters are read back below; the next chunk's are fresh
+        }
+        n_counts = p;
+    }
+    e->last_tail_passes = tail ? n_counts : 0;
     // per chain: select(0); then per iteration: evaluate(it), expand(it)+select(it+1)
     // fused, and expand alone after the last evaluation.  Timer 0 samples the
     // select-bearing launch (k_select / k_expand_select), 2 the last k_expand.
-    for (uint32_t it = 0; it < num_searches; ++it) {
+    for (uint32_t it = 0; it < (tail ? 0u : num_searches); ++it) {
         for (int h = 0; h < nchain; ++h) {
             const hipStream_t sh = e->chain_stream[h];
             const BatchView bv = batch_view(e, h, it);
@@ -501,7 +597,7 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
             const bool sample = timed && (it % e->timer.stride == 0);
             if (it == 0) {
                 if (sample) SPAI_TRY(timer_record(e, 0, it, true, sh, h));
-                k_select<<<g8, kBlock, 0, sh>>>(tv, bv, act, nh, e->cfg.c, e->err.p);
+                k_select<false><<<g8, kBlock, 0, sh>>>(tv, bv, act, nh, e->cfg.c, e->err.p);
                 if (sample) SPAI_TRY(timer_record(e, 0, it, false, sh, h));
             }
             if (sample) SPAI_TRY(timer_record(e, 1, it, true, sh, h));
@@ -515,8 +611,8 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
             if (it + 1 < num_searches) {
                 const bool s2 = timed && ((it + 1) % e->timer.stride == 0);
                 if (s2) SPAI_TRY(timer_record(e, 0, it + 1, true, sh, h));
-                k_expand_select<<<g8, kBlock, 0, sh>>>(tv, bv, batch_view(e, h, it + 1), act, nh, e->cfg.c,
-                                                       e->err.p);
+                k_expand_select<false><<<g8, kBlock, 0, sh>>>(tv, bv, batch_view(e, h, it + 1), act, nh,
+                                                              e->cfg.c, e->err.p);
                 if (s2) SPAI_TRY(timer_record(e, 0, it + 1, false, sh, h));
             } else {
                 if (sample) SPAI_TRY(timer_record(e, 2, it, true, sh, h));
@@ -532,18 +628,18 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
     }
     k_root_stats<<<(n + 255) / 256, 256, 0, st>>>(tv, e->active.p, n, e->stats.p);
     SPAI_HIP(hipGetLastError());
-    std::vector<uint32_t> stats((size_t)n * 8), counts(num_searches), ch_counts((size_t)nchain * num_searches);
+    std::vector<uint32_t> stats((size_t)n * 8), counts(n_counts), ch_counts((size_t)nchain * n_counts);
     uint32_t err = 0;
     SPAI_HIP(hipMemcpyAsync(stats.data(), e->stats.p, stats.size() * 4, hipMemcpyDeviceToHost, st));
-    if (num_searches)
+    if (n_counts)
         for (int h = 0; h < nchain; ++h)
-            SPAI_HIP(hipMemcpyAsync(ch_counts.data() + (size_t)h * num_searches, e->batch[h].iter_counts.p,
-                                    num_searches * 4, hipMemcpyDeviceToHost, st));
+            SPAI_HIP(hipMemcpyAsync(ch_counts.data() + (size_t)h * n_counts, e->batch[h].iter_counts.p,
+                                    n_counts * 4, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipMemcpyAsync(&err, e->err.p, 4, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipStreamSynchronize(st));
-    SPAI_TRY(timer_collect(e, ch_counts, num_searches, cnt));
+    SPAI_TRY(timer_collect(e, ch_counts, n_counts, cnt));
     for (int h = 0; h < nchain; ++h)
-        for (uint32_t i = 0; i < num_searches; ++i) counts[i] += ch_counts[(size_t)h * num_searches + i];
+        for (uint32_t i = 0; i < n_counts; ++i) counts[i] += ch_counts[(size_t)h * n_counts + i];
     SPAI_CHECK(!(err & kErrCapacity), SPAI_ERR_CAPACITY, "node arena full (cap %u per tree)", T.cap);
     SPAI_CHECK(!(err & kErrDepth), SPAI_ERR_CAPACITY, "tree deeper than %d", kMaxDepth);
     SPAI_CHECK(!(err & kErrNan), SPAI_ERR_NAN, "NaN UCB in select (reference: partial_cmp().unwrap() panics)");
@@ -707,10 +803,12 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
             }
         }
         SPAI_TRY(upload_roots(e, 0, T.n_trees));
-        if (trace)   // move, active trees, leaves evaluated, search seconds, host seconds (sampling + root upload)
-            std::fprintf(trace, "%llu,%u,%.0f,%.6f,%.6f\n", (unsigned long long)move_no, na, ev,
+        if (trace)   // move, active trees, leaves evaluated, search seconds, host seconds (sampling + root
+                     // upload), search passes (tail mode; 0: one launch pair per iteration)
+            std::fprintf(trace, "%llu,%u,%.0f,%.6f,%.6f,%u\n", (unsigned long long)move_no, na, ev,
                          std::chrono::duration<double>(tm1 - tm0).count(),
-                         std::chrono::duration<double>(std::chrono::steady_clock::now() - tm1).count());
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - tm1).count(),
+                         e->last_tail_passes);
         ++move_no;
     }
     if (trace) std::fclose(trace);

@@ -82,6 +82,7 @@ struct Trees {
     DevBuf<uint32_t> path;          // [n_trees * kMaxDepth]
     DevBuf<uint8_t> depth;          // [n_trees]
     DevBuf<uint32_t> slot;          // [n_trees] leaf slot in the current batch (select -> expand)
+    DevBuf<uint32_t> left;          // [n_trees] search iterations left (tail run-on mode, search.hip)
     // host mirrors of the root bookkeeping
     std::vector<uint32_t> h_root;
     std::vector<c4::State> h_root_state;
@@ -196,6 +197,7 @@ struct spai_engine {
     hipStream_t chain_stream[kChains] = {nullptr, nullptr, nullptr, nullptr};
     hipEvent_t ev_fork = nullptr, ev_join[kChains] = {nullptr, nullptr, nullptr, nullptr};
     double last_evals_per_iter = -1;   // previous search call's mean leaves per iteration (< 0: none yet)
+    uint32_t last_tail_passes = 0;     // previous search call's tail-mode passes (0: not in tail mode)
     spai_net *net = nullptr;
     spai::DevBuf<uint32_t> active;   // active tree list
     spai::DevBuf<uint32_t> err;      // device error flags

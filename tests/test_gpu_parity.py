@@ -404,6 +404,39 @@ def test_self_play_hash_matches_oracle(spai, oracle):
     e.close()
 
 
+def test_self_play_tail_mode_matches_oracle(spai, oracle, tmp_path):
+    """the tail mode (search.hip select_tree RUN_ON): once a search call averages
+    fewer than 64 leaves per iteration, the next one lets every tree run its
+    iterations on through terminal leaves inside one launch.  Self-play with the
+    hash evaluator on 48 games (one search chain) must still equal the oracle's
+    sample stream bit for bit, and the per-move trace must show tail-mode moves
+    (a sixth column of search passes) that used far fewer passes than iterations"""
+    n, sims, seed = 48, 96, 23
+    trace = tmp_path / "moves.csv"
+    os.environ["SPAI_TRACE_MOVES"] = str(trace)
+    try:
+        e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_HASH, seed=seed)
+        games, stats = e.self_play(n)
+        e.close()
+    finally:
+        del os.environ["SPAI_TRACE_MOVES"]
+    ref = oracle.self_play(oracle.GAME_CONNECT4, n, sims, seed, eval_kind=oracle.EVAL_HASH, max_plies=42)
+    k = 0
+    for g in games:
+        m = len(g["value"])
+        assert list(ref["game"][k:k + m]) == [g["game"]] * m
+        np.testing.assert_array_equal(g["policy"], ref["policy"][k:k + m])
+        np.testing.assert_array_equal(g["value"], ref["value"][k:k + m])
+        np.testing.assert_array_equal(g["enc"], ref["enc"][k:k + m])
+        assert list(g["moves"]) == list(ref["moves"][g["game"], :m])
+        k += m
+    assert k == len(ref["value"]) and stats["sims"] == ref["sims"]
+    rows = [[float(v) for v in l.split(",")] for l in trace.read_text().splitlines()]
+    tail = [r for r in rows if r[5] > 0]
+    assert tail, "no move ran in tail mode"
+    assert min(r[5] for r in tail) < sims / 4, [r[5] for r in tail]   # passes, not one per iteration
+
+
 def test_self_play_net_properties(spai, oracle):
     """bf16 net self-play: every game is a legal Connect4 game ending in the
     recorded outcome; values are +-1/0 by perspective; policies are normalised."""
