@@ -369,7 +369,16 @@ __global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict
     }
 }
 
-// dW[n][c][tap] = sum_chunk part[chunk][n][tap * cinp + c]  (fixed order)
+// dW[n][c][tap] = sum_chunk part[chunk][n][tap * cinp + c]  (fixed order).  At
+// batch 128 there are 32 chunks: all 32 loads in flight at once, and 64-thread
+// workgroups (576 of them for 64 x 64, instead of 144 of 256 threads on 256 CUs)
+#ifndef SPAI_WG_REDUCE_BATCH
+#define SPAI_WG_REDUCE_BATCH 32
+#endif
+#ifndef SPAI_WG_REDUCE_THREADS
+#define SPAI_WG_REDUCE_THREADS 64
+#endif
+constexpr int kWgReduceBatch = SPAI_WG_REDUCE_BATCH, kWgReduceThreads = SPAI_WG_REDUCE_THREADS;
 __global__ void k_wgrad_reduce(const float *__restrict__ part, int B, int cin, int cout, float *__restrict__ dw) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int cinp = round4(cin), K = 9 * cinp;
@@ -379,12 +388,12 @@ __global__ void k_wgrad_reduce(const float *__restrict__ part, int B, int cin, i
             const float *src = part + i;
             const size_t stride = (size_t)cout * K;
             float s = 0.f;
-            for (int b0 = 0; b0 < B; b0 += 16) {   // 16 loads in flight, summed in batch order
-                float v[16];
+            for (int b0 = 0; b0 < B; b0 += kWgReduceBatch) {   // kWgReduceBatch loads in flight, summed in batch order
+                float v[kWgReduceBatch];
 #pragma unroll
-                for (int j = 0; j < 16; ++j) v[j] = b0 + j < B ? src[(size_t)(b0 + j) * stride] : 0.f;
+                for (int j = 0; j < kWgReduceBatch; ++j) v[j] = b0 + j < B ? src[(size_t)(b0 + j) * stride] : 0.f;
 #pragma unroll
-                for (int j = 0; j < 16; ++j)
+                for (int j = 0; j < kWgReduceBatch; ++j)
                     if (b0 + j < B) s += v[j];
             }
             dw[((size_t)n * cin + c) * 9 + tap] = s;
@@ -762,7 +771,8 @@ int launch_wgrad(float *wpart, const float *x, int cin, const float *dz, int cou
     case 64: k_wgrad_mfma<64><<<grid, kThreads, lds, st>>>(x, cin, dz, cout, B, groups, wpart); break;
     default: set_error("learner wgrad: %d input channels not built", cin); return SPAI_ERR_UNSUPPORTED;
     }
-    k_wgrad_reduce<<<blocks_of((size_t)cout * 9 * cinp), kThreads, 0, st>>>(wpart, chunks, cin, cout, dw);
+    k_wgrad_reduce<<<blocks_of((size_t)cout * 9 * cinp, kWgReduceThreads), kWgReduceThreads, 0, st>>>(wpart, chunks, cin,
+                                                                                                     cout, dw);
     return SPAI_OK;
 }
 

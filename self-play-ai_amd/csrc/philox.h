@@ -11,6 +11,7 @@
 #include <stdint.h>
 
 #include <cmath>
+#include <vector>
 
 namespace spai {
 
@@ -38,12 +39,31 @@ inline double sample_uniform(uint64_t seed, uint64_t game_id, uint64_t move_no) 
 }
 
 // index of the sampled child, -1 if n is out of range, -2 if all weights are 0
-inline int weighted_index(const float *visits, int n, float temperature, double u) {
+// visits^temperature for the integer visit counts of a self-play run, each
+// computed once by the same std::pow (so the weights are the same bits); any
+// other value goes to std::pow directly
+struct PowCache {
+    double temperature = -1.0;
+    std::vector<double> tab;
+    double operator()(float v, float t) {
+        if ((double)t != temperature) {
+            temperature = (double)t;
+            tab.clear();
+        }
+        if (!(v >= 0.f) || v >= 1.0e6f || v != (float)(uint32_t)v) return std::pow((double)v, (double)t);
+        const uint32_t k = (uint32_t)v;
+        while (tab.size() <= k) tab.push_back(std::pow((double)tab.size(), (double)t));
+        return tab[k];
+    }
+};
+
+template <class Pow>
+inline int weighted_index_with(const float *visits, int n, float temperature, double u, Pow &&pw) {
     double cum[512];
     double total = 0.0;
     if (n <= 0 || n > 512) return -1;
     for (int i = 0; i < n; ++i) {
-        total += std::pow((double)visits[i], (double)temperature);
+        total += pw(visits[i], temperature);
         cum[i] = total;
     }
     if (!(total > 0.0)) return -2;
@@ -54,6 +74,11 @@ inline int weighted_index(const float *visits, int n, float temperature, double 
         if (i == 0 ? cum[0] > 0.0 : cum[i] > cum[i - 1]) last = i;
     }
     return last;   // u * total rounded up to total
+}
+
+inline int weighted_index(const float *visits, int n, float temperature, double u) {
+    return weighted_index_with(visits, n, temperature, u,
+                               [](float v, float t) { return std::pow((double)v, (double)t); });
 }
 
 }  // namespace spai

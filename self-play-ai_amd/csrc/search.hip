@@ -66,10 +66,14 @@ struct BatchView {
 
 // PUCT score, mcts.rs:91-100, evaluated in the reference's operation order
 // (no contraction: built with -ffp-contract=off; sqrt and / correctly rounded).
+// The quotient is computed for every child and selected (an unvisited child has
+// q = 0): under a branch the compiler sank the load of the record's value sum
+// into it, which put a second dependent memory round trip on every level.
 __device__ __forceinline__ float ucb(uint32_t n_parent, const uint4 &ch, float c) {
     const uint32_t n = ch.x;
     const float w = __uint_as_float(ch.y), prior = __uint_as_float(ch.z);
-    const float q = n == 0 ? 0.0f : ((-w / (float)n) + 1.0f) / 2.0f;
+    const float qv = ((-w / (float)(n == 0 ? 1u : n)) + 1.0f) / 2.0f;
+    const float q = n == 0 ? 0.0f : qv;
     float u = c * prior;
     u = u * sqrtf((float)n_parent);
     u = u / (1.0f + (float)n);
@@ -78,15 +82,70 @@ __device__ __forceinline__ float ucb(uint32_t n_parent, const uint4 &ch, float c
 
 // backprop (mcts.rs:145-159) over path[0..d]: level d is the leaf (+v), signs
 // alternate upward; lane l of the 8-lane group updates the levels == l (mod 8)
-__device__ __forceinline__ void backup_level(uint4 *nodes, uint32_t node, int d, int lvl, float v) {
-    uint4 *nd = nodes + node;
-    const float sign = ((d - lvl) & 1) ? -1.0f : 1.0f;
-    nd->x = nd->x + 1u;
-    nd->y = __float_as_uint(__uint_as_float(nd->y) + sign * v);
+// (at most kMaxDepth / 8 = 6 per lane).  The nodes of a path are distinct, so a
+// lane loads all of its levels' records first and then stores them: one memory
+// round trip, where a load-add-store per level (the compiler cannot reorder a
+// level's load above the previous level's store) paid one per level.
+constexpr int kLevelsPerLane = kMaxDepth / kLanesPerTree;
+// (The loads are unconditional -- levels past d read the path's root, whose node
+// exists -- so that no branch separates them: hipcc waits vmcnt(0) at each one.)
+__device__ __forceinline__ void backup_nodes(uint4 *nodes, const uint32_t (&node)[kLevelsPerLane], int d, float v,
+                                             int lane8) {
+    uint2 r[kLevelsPerLane];
+#pragma unroll
+    for (int j = 0; j < kLevelsPerLane; ++j) r[j] = *(const uint2 *)(nodes + (lane8 + 8 * j <= d ? node[j] : node[0]));
+#pragma unroll
+    for (int j = 0; j < kLevelsPerLane; ++j) {
+        const int lvl = lane8 + 8 * j;
+        if (lvl <= d) {
+            const float sign = ((d - lvl) & 1) ? -1.0f : 1.0f;
+            *(uint2 *)(nodes + node[j]) = make_uint2(r[j].x + 1u, __float_as_uint(__uint_as_float(r[j].y) + sign * v));
+        }
+    }
 }
 
+// the same from the path recorded in memory (expand: the select was an earlier launch)
 __device__ __forceinline__ void backup(uint4 *nodes, const uint32_t *path, int d, float v, int lane8) {
-    for (int lvl = lane8; lvl <= d; lvl += kLanesPerTree) backup_level(nodes, path[lvl], d, lvl, v);
+    uint32_t node[kLevelsPerLane];
+#pragma unroll
+    for (int j = 0; j < kLevelsPerLane; ++j) node[j] = path[lane8 + 8 * j <= d ? lane8 + 8 * j : 0];
+    backup_nodes(nodes, node, d, v, lane8);
+}
+
+// the column of child k (the k-th open column; 0 when k >= the open count),
+// without kth_bit's data-dependent loop
+__device__ __forceinline__ int lane_column(uint32_t open, int k) {
+#pragma unroll
+    for (int i = 0; i < c4::kActions - 1; ++i) open = i < k ? open & (open - 1u) : open;
+    return open ? __builtin_ctz(open) : 0;
+}
+
+// a tree's best child so far in the argmax over its 8 lanes: score, index, record, action
+struct Winner {
+    float u;
+    int i;
+    uint4 rec;
+    int col;
+};
+template <int CTRL>
+__device__ __forceinline__ int dpp(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+// one butterfly step: take the partner lane's candidate if its score is larger,
+// or equal with a larger index (ties go to the last child)
+template <int CTRL>
+__device__ __forceinline__ void dpp_argmax_step(Winner &w) {
+    const float ou = __int_as_float(dpp<CTRL>(__float_as_int(w.u)));
+    const int oi = dpp<CTRL>(w.i);
+    const uint4 orec = make_uint4((uint32_t)dpp<CTRL>((int)w.rec.x), (uint32_t)dpp<CTRL>((int)w.rec.y),
+                                  (uint32_t)dpp<CTRL>((int)w.rec.z), (uint32_t)dpp<CTRL>((int)w.rec.w));
+    const int ocol = dpp<CTRL>(w.col);
+    if (ou > w.u || (ou == w.u && oi > w.i)) {
+        w.u = ou;
+        w.i = oi;
+        w.rec = orec;
+        w.col = ocol;
+    }
 }
 
 // One PUCT descent of tree t (mcts.rs:235-250) by its 8 lanes.  A terminal leaf
@@ -123,24 +182,19 @@ __device__ __forceinline__ Descent descend(const TreeView &T, uint32_t t, int la
             if (lane8 == 0) atomicOr(err, kErrNan);
             return kError;
         }
-        // argmax with ties to the LAST child (Iterator::max_by, mcts.rs:110-113)
-        float bu = u;
-        int bi = lane8;
-#pragma unroll
-        for (int m = 1; m < kLanesPerTree; m <<= 1) {
-            const float ou = __shfl_xor(bu, m, kLanesPerTree);
-            const int oi = __shfl_xor(bi, m, kLanesPerTree);
-            if (ou > bu || (ou == bu && oi > bi)) {
-                bu = ou;
-                bi = oi;
-            }
-        }
-        rec.x = __shfl(ch.x, bi, kLanesPerTree);
-        rec.y = __shfl(ch.y, bi, kLanesPerTree);
-        rec.z = __shfl(ch.z, bi, kLanesPerTree);
-        rec.w = __shfl(ch.w, bi, kLanesPerTree);
-        // replay the child's action on the bitboards (children are in legal-action order)
-        const int a = c4::kth_bit(c4::open_columns(x | o), bi);
+        // argmax with ties to the LAST child (Iterator::max_by, mcts.rs:110-113) as a
+        // butterfly of DPP moves over the tree's 8 lanes, carrying the winner's record
+        // and its action (children are in legal-action order: child k plays the k-th
+        // open column) along, so no lane shuffle through the LDS crossbar sits on the
+        // descent's dependent chain
+        Winner w{u, lane8, ch, lane_column(c4::open_columns(x | o), lane8)};
+        dpp_argmax_step<0xB1>(w);    // quad_perm [1,0,3,2]: lane ^ 1
+        dpp_argmax_step<0x4E>(w);    // quad_perm [2,3,0,1]: lane ^ 2
+        dpp_argmax_step<0x141>(w);   // row_half_mirror: lane i <-> 7 - i of the 8, across the two quads
+        const int bi = w.i;
+        rec = w.rec;
+        // replay the child's action on the bitboards
+        const int a = w.col;
         const uint64_t bit = c4::drop_bit(x | o, a);
         uint64_t mover;
         if (c4::x_to_move(n)) { x |= bit; mover = x; }
@@ -167,13 +221,8 @@ __device__ __forceinline__ Descent descend(const TreeView &T, uint32_t t, int la
     }
     if (lane8 == 0) T.depth[t] = (uint8_t)d;
     if (status != c4::kOngoing) {                           // terminal leaf: backprop(leaf, value), mcts.rs:245-247
-        const float v = c4::terminal_value(status);
-        const uint32_t pr[6] = {p0, p1, p2, p3, p4, p5};
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            const int lvl = lane8 + 8 * j;
-            if (lvl <= d) backup_level(nodes, pr[j], d, lvl, v);
-        }
+        const uint32_t pr[kLevelsPerLane] = {p0, p1, p2, p3, p4, p5};
+        backup_nodes(nodes, pr, d, c4::terminal_value(status), lane8);
         return kTerminal;
     }
     return kLive;
@@ -353,8 +402,12 @@ BatchView batch_view(spai_engine *e, int chain, uint32_t it) {
 // for A/B measurements.)  The split never changes results: trees are independent.
 constexpr double kMinChainLeaves = 64;
 // tail mode (select_tree RUN_ON) below this many leaves per iteration in the
-// previous search call; host checks for the end every kTailChunk passes
-constexpr double kTailLeaves = 64;
+// previous search call; host checks for the end every kTailChunk passes.  A pass
+// lasts as long as its longest terminal run (~3 us per descent), so the mode only
+// pays when hardly any tree still needs evaluations: at 34 and 6.6 leaves per
+// iteration (moves 36 and 37 of a bench step) it took 114 and 49 ms against
+// ~25 and ~18 ms for one launch pair per iteration (profiles/r04/tail)
+constexpr double kTailLeaves = 0.05;
 constexpr uint32_t kTailChunk = 4;
 static int env_int(const char *name, int dflt) {
     const char *v = std::getenv(name);
@@ -532,7 +585,8 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
     // tail mode (select_tree RUN_ON): late in a game, when the previous search call
     // of these trees evaluated fewer than SPAI_TAIL_LEAVES leaves per iteration
     // (a single chain then); 0 turns it off
-    static const double tail_leaves = env_int("SPAI_TAIL_LEAVES", (int)kTailLeaves);
+    const char *tl_env = std::getenv("SPAI_TAIL_LEAVES");   // read per call: tests set it per case
+    const double tail_leaves = tl_env ? std::atof(tl_env) : kTailLeaves;
     const bool tail = nchain == 1 && num_searches > 0 && e->last_evals_per_iter >= 0 &&
                       e->last_evals_per_iter < tail_leaves;
     for (int h = 0; h < nchain; ++h) {   // per-iteration leaf counters (also the batch slot counters)
@@ -744,6 +798,7 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
     std::vector<float> enc, sp, sv;
     double sims = 0, evals = 0, games = 0, positions = 0, moves = 0;
     uint64_t move_no = 0;
+    PowCache pow_cache;   // visits^T of the sampling, once per visit count (was ~0.5 ms of std::pow per move)
     // optional per-move trace (diagnostics): SPAI_TRACE_MOVES=<csv path>
     FILE *trace = nullptr;
     if (const char *tp = std::getenv("SPAI_TRACE_MOVES")) trace = std::fopen(tp, "a");
@@ -760,7 +815,7 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
             const uint32_t t = active[k];
             Hist &h = hist[t];
             const double u = sample_uniform(e->cfg.seed, gid_base + t, move_no);
-            const int idx = weighted_index(vis.data() + (size_t)k * 7, (int)nch[k], e->cfg.temperature, u);
+            const int idx = weighted_index_with(vis.data() + (size_t)k * 7, (int)nch[k], e->cfg.temperature, u, pow_cache);
             SPAI_CHECK(idx >= 0, SPAI_ERR_NAN, "WeightedIndex over all-zero visit counts (game %u)", t);
             const c4::State rs = T.h_root_state[t];
             const int a = c4::kth_bit(c4::legal_mask(rs.x, rs.o, rs.status), idx);
@@ -772,9 +827,9 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
             if (cs.status != c4::kOngoing) {                  // is_terminal: emit, trees_vec.remove(i)
                 const float v = c4::terminal_value(cs.status);
                 const size_t m = h.states.size();
-                enc.assign(m * 126, 0.f);
+                enc.assign(sink ? m * 126 : 0, 0.f);
                 sv.resize(m);
-                for (size_t j = 0; j < m; ++j) {
+                for (size_t j = 0; j < (sink ? m : 0); ++j) {
                     const c4::State &s = h.states[j];
                     const bool xm = c4::x_to_move(s.n);
                     const uint64_t mine = xm ? s.x : s.o, theirs = xm ? s.o : s.x;

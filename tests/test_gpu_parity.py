@@ -404,22 +404,31 @@ def test_self_play_hash_matches_oracle(spai, oracle):
     e.close()
 
 
-def test_self_play_tail_mode_matches_oracle(spai, oracle, tmp_path):
+kTailChunk = 4   # search.hip: passes per host check
+
+
+@pytest.mark.parametrize("tail_leaves", [None, "64"])
+def test_self_play_tail_mode_matches_oracle(spai, oracle, tmp_path, tail_leaves):
     """the tail mode (search.hip select_tree RUN_ON): once a search call averages
-    fewer than 64 leaves per iteration, the next one lets every tree run its
-    iterations on through terminal leaves inside one launch.  Self-play with the
-    hash evaluator on 48 games (one search chain) must still equal the oracle's
-    sample stream bit for bit, and the per-move trace must show tail-mode moves
-    (a sixth column of search passes) that used far fewer passes than iterations"""
+    fewer than SPAI_TAIL_LEAVES leaves per iteration (default 0.05), the next one
+    lets every tree run its iterations on through terminal leaves inside one
+    launch.  Self-play with the hash evaluator on 48 games (one search chain)
+    must still equal the oracle's sample stream bit for bit -- at the default and
+    at 64, where tail-mode moves still hold trees that need evaluations -- and the
+    per-move trace must show tail-mode moves (a sixth column of search passes)"""
     n, sims, seed = 48, 96, 23
     trace = tmp_path / "moves.csv"
-    os.environ["SPAI_TRACE_MOVES"] = str(trace)
+    env = {"SPAI_TRACE_MOVES": str(trace)}
+    if tail_leaves:
+        env["SPAI_TAIL_LEAVES"] = tail_leaves
+    os.environ.update(env)
     try:
         e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_HASH, seed=seed)
         games, stats = e.self_play(n)
         e.close()
     finally:
-        del os.environ["SPAI_TRACE_MOVES"]
+        for k in env:
+            del os.environ[k]
     ref = oracle.self_play(oracle.GAME_CONNECT4, n, sims, seed, eval_kind=oracle.EVAL_HASH, max_plies=42)
     k = 0
     for g in games:
@@ -435,6 +444,8 @@ def test_self_play_tail_mode_matches_oracle(spai, oracle, tmp_path):
     tail = [r for r in rows if r[5] > 0]
     assert tail, "no move ran in tail mode"
     assert min(r[5] for r in tail) < sims / 4, [r[5] for r in tail]   # passes, not one per iteration
+    if tail_leaves:   # a tail move whose trees still needed evaluations (more than one pass)
+        assert max(r[5] for r in tail) > kTailChunk, [r[5] for r in tail]
 
 
 def test_self_play_net_properties(spai, oracle):
