@@ -148,20 +148,30 @@ __device__ __forceinline__ void dpp_argmax_step(Winner &w) {
     }
 }
 
+// a tree's root for this search call: node id and position (constant while it runs)
+struct RootInfo {
+    uint32_t node;
+    uint64_t x, o;
+    uint8_t n, status;
+};
+__device__ __forceinline__ RootInfo load_root(const TreeView &T, uint32_t t) {
+    return RootInfo{T.root[t], T.root_x[t], T.root_o[t], T.root_n[t], T.root_status[t]};
+}
+
 // One PUCT descent of tree t (mcts.rs:235-250) by its 8 lanes.  A terminal leaf
 // is backed up in place (mcts.rs:245-247) and kTerminal returned; a live leaf is
 // returned as kLive with its position in (x, o, n) and its path recorded (T.path,
 // T.depth); kError after a NaN UCB or an over-deep path (flag set in err).
 enum Descent { kTerminal = 0, kLive = 1, kError = 2 };
-__device__ __forceinline__ Descent descend(const TreeView &T, uint32_t t, int lane8, float c, uint32_t *err,
-                                           uint64_t &x, uint64_t &o, uint8_t &n) {
+__device__ __forceinline__ Descent descend(const TreeView &T, uint32_t t, const RootInfo &root, int lane8, float c,
+                                           uint32_t *err, uint64_t &x, uint64_t &o, uint8_t &n) {
     uint4 *nodes = T.nodes + (size_t)t * T.cap;
     uint32_t *path = T.path + (size_t)t * kMaxDepth;
-    uint32_t node = T.root[t];
-    x = T.root_x[t];
-    o = T.root_o[t];
-    n = T.root_n[t];
-    uint8_t status = T.root_status[t];
+    uint32_t node = root.node;
+    x = root.x;
+    o = root.o;
+    n = root.n;
+    uint8_t status = root.status;
     uint4 rec = nodes[node];
     // path levels == lane8 (mod 8) kept in this lane's registers (kMaxDepth = 6 x 8)
     uint32_t p0 = node, p1 = 0, p2 = 0, p3 = 0, p4 = 0, p5 = 0;
@@ -252,19 +262,19 @@ __device__ __forceinline__ void slot_leaf(const TreeView &T, const BatchView &B,
 // then lasts as long as its longest terminal run, which pays off only late in a
 // game, where most iterations need no evaluation.
 template <bool RUN_ON>
-__device__ __forceinline__ void select_tree(const TreeView &T, const BatchView &B, uint32_t t, int lane8, float c,
-                                            uint32_t *err) {
+__device__ __forceinline__ void select_tree(const TreeView &T, const BatchView &B, uint32_t t, const RootInfo &root,
+                                            int lane8, float c, uint32_t *err) {
     if (lane8 == 0) T.slot[t] = kNoSlot;
     uint64_t x, o;
     uint8_t n;
     if (!RUN_ON) {
-        if (descend(T, t, lane8, c, err, x, o, n) == kLive) slot_leaf(T, B, t, lane8, x, o, n);
+        if (descend(T, t, root, lane8, c, err, x, o, n) == kLive) slot_leaf(T, B, t, lane8, x, o, n);
         return;
     }
     uint32_t left = T.left[t];
     while (left > 0) {
         --left;
-        const Descent r = descend(T, t, lane8, c, err, x, o, n);
+        const Descent r = descend(T, t, root, lane8, c, err, x, o, n);
         if (r == kLive) slot_leaf(T, B, t, lane8, x, o, n);
         if (r != kTerminal) break;
         // the next descent reads records the other lanes of this tree just backed
@@ -275,32 +285,44 @@ __device__ __forceinline__ void select_tree(const TreeView &T, const BatchView &
 }
 
 // expand leaf slot s of batch B (mcts.rs:116-143) and back its value up (:145-159)
-__device__ __forceinline__ void expand_leaf(const TreeView &T, const BatchView &B, uint32_t s, int lane8,
+// Everything the expansion reads is issued together (one memory round trip after
+// the slot): the leaf's depth, every path level this lane backs up (entries past
+// the depth are stale and unused), the leaf position, the arena fill, this lane's
+// prior and the value.  The leaf is path[d], which lane d & 7 already holds.
+__device__ __forceinline__ void expand_leaf(const TreeView &T, const BatchView &B, uint32_t t, uint32_t s, int lane8,
                                             uint32_t *err) {
-    const uint32_t t = B.tree[s];
     uint4 *nodes = T.nodes + (size_t)t * T.cap;
     const uint32_t *path = T.path + (size_t)t * kMaxDepth;
     const int d = T.depth[t];
-    const uint32_t leaf = path[d];
+    uint32_t lv[kLevelsPerLane];
+#pragma unroll
+    for (int j = 0; j < kLevelsPerLane; ++j) lv[j] = path[lane8 + 8 * j];
     const uint64_t occ = B.mine[s] | B.theirs[s];
+    const uint32_t first = T.next_free[t];
+    const float prior = B.priors[(size_t)s * kPriorStride + lane8];   // lane 7: the stride's padding
+    const float value = B.value[s];
     // legal actions of the (live) leaf; children in ascending action order (mcts.rs:116-143)
     const bool legal = lane8 < c4::kActions && !((occ >> (7 * lane8 + 5)) & 1ull);
     const uint64_t ball = __ballot(legal);
     const uint32_t grp = (uint32_t)(ball >> (threadIdx.x & 63 & ~(kLanesPerTree - 1))) & 0xFFu;
     const uint32_t nch = c4::popc32(grp);
     const uint32_t idx = c4::popc32(grp & ((1u << lane8) - 1u));
-    const uint32_t first = T.next_free[t];
     if (first + nch > T.cap) {
         if (lane8 == 0) atomicOr(err, kErrCapacity);
         return;
     }
-    if (legal) nodes[first + idx] = make_uint4(0u, 0u, __float_as_uint(B.priors[(size_t)s * kPriorStride + lane8]),
-                                               kNoChildren);
-    if (lane8 == 0) {
-        T.next_free[t] = first + nch;
+    if (legal) nodes[first + idx] = make_uint4(0u, 0u, __float_as_uint(prior), kNoChildren);
+    if (lane8 == 0) T.next_free[t] = first + nch;
+    uint32_t node[kLevelsPerLane];   // this lane's levels of the path; 0 (a valid dummy) past the depth
+#pragma unroll
+    for (int j = 0; j < kLevelsPerLane; ++j) node[j] = lane8 + 8 * j <= d ? lv[j] : 0u;
+    if (lane8 == (d & 7)) {
+        uint32_t leaf = node[0];
+#pragma unroll
+        for (int j = 1; j < kLevelsPerLane; ++j) leaf = (d >> 3) == j ? node[j] : leaf;
         nodes[leaf].w = first | (nch << 24);
     }
-    backup(nodes, path, d, B.value[s], lane8);
+    backup_nodes(nodes, node, d, value, lane8);
 }
 
 template <bool RUN_ON>
@@ -311,7 +333,8 @@ __global__ __launch_bounds__(kBlock) void k_select(TreeView T, BatchView B, cons
     __builtin_amdgcn_s_setprio(SPAI_TREE_PRIO);   // experiment: issue priority against the co-resident forward
 #endif
     if (gi >= n_active) return;
-    select_tree<RUN_ON>(T, B, active[gi], threadIdx.x & (kLanesPerTree - 1), c, err);
+    const uint32_t t = active[gi];
+    select_tree<RUN_ON>(T, B, t, load_root(T, t), threadIdx.x & (kLanesPerTree - 1), c, err);
 }
 
 // expand this iteration's leaf of every tree (batch `cur`), then select the next
@@ -330,9 +353,10 @@ __global__ __launch_bounds__(kBlock) void k_expand_select(TreeView T, BatchView 
     const int lane8 = threadIdx.x & (kLanesPerTree - 1);
     const uint32_t t = active[gi];
     const uint32_t s = T.slot[t];
-    if (s != kNoSlot) expand_leaf(T, cur, s, lane8, err);
+    const RootInfo root = load_root(T, t);   // read-only during the search: loaded with the slot, off the chain
+    if (s != kNoSlot) expand_leaf(T, cur, t, s, lane8, err);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    select_tree<RUN_ON>(T, nxt, t, lane8, c, err);
+    select_tree<RUN_ON>(T, nxt, t, root, lane8, c, err);
 }
 
 // tail mode: every active tree has all `iters` iterations of this search call ahead
@@ -357,7 +381,7 @@ __global__ __launch_bounds__(kBlock) void k_eval_stub(BatchView B, uint32_t max_
 __global__ __launch_bounds__(kBlock) void k_expand(TreeView T, BatchView B, uint32_t max_n, uint32_t *err) {
     const uint32_t s = (blockIdx.x * blockDim.x + threadIdx.x) / kLanesPerTree;
     if (s >= max_n || s >= *B.count) return;
-    expand_leaf(T, B, s, threadIdx.x & (kLanesPerTree - 1), err);
+    expand_leaf(T, B, B.tree[s], s, threadIdx.x & (kLanesPerTree - 1), err);
 }
 
 // per active tree: [0] = root first|nch<<24 (children word), [1..7] child visit counts
