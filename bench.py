@@ -307,6 +307,7 @@ def main():
                                % (G, args.sims, args.blocks),
                    "model": "c4-resnet-%dx64" % args.blocks, "games_per_gpu": G, "sims_per_move": args.sims,
                    "global_batch": G * dist.world, "parallelism": "dp%d (games sharded, no collective)" % dist.world},
+        "work": {"sims": sims, "games": games, "evals": evals, "positions": positions},   # summed over ranks
         "evals_per_sec": evals / dt_max,
         "positions_per_sec": positions / dt_max,
         "kernel_ms": {k: v["avg_ms"] for k, v in timing.items()},

@@ -18,6 +18,8 @@ test_gpu_fp32.py at smaller sizes).
 * C5 with several self-play workers on one device (main.rs:169-186 runs 6):
   three workers' pushes interleave in the ring, checked the same way.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -108,3 +110,47 @@ def test_c5_pipeline_several_workers_one_device(spai, tmp_path):
     for it in range(4):
         p = spai.load_params(str(tmp_path / ("%d.safetensors" % it)), 2)
         assert np.isfinite(p).all()
+
+
+def test_bench_two_ranks_one_gpu(tmp_path):
+    """bench.py's N > 1 path with libspai in both ranks: two rank processes on the
+    one GPU (RANK / WORLD_SIZE / MASTER_* as torch.distributed.run sets them,
+    SPAI_BENCH_DEVICE=0), each playing its shard of game ids, the host group's
+    barrier and max/sum reductions.  Games are independent and a position's
+    evaluation does not depend on its batch, so the summed work of 2 ranks x G
+    games equals one rank's 2G games exactly: simulations, evaluations,
+    finished games and positions"""
+    import json
+    import socket
+    import subprocess
+    import sys
+    from conftest import REPO
+    G = 96
+    args = ["--sims", "32", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-isolated",
+            "--no-rules-bench", "--no-chess", "--no-timing"]
+    base = dict(os.environ, SPAI_BENCH_DEVICE="0")
+
+    def run(world, games):
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        env = dict(base, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SPAI_GROUP_PORT=str(port),
+                   WORLD_SIZE=str(world))
+        procs = [subprocess.Popen([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(world),
+                                   "--games", str(games)] + args,
+                                  env=dict(env, RANK=str(r), LOCAL_RANK=str(r)), stdout=subprocess.PIPE,
+                                  stderr=subprocess.PIPE, text=True) for r in range(world)]
+        try:
+            outs = [p.communicate(timeout=240) for p in procs]
+        finally:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        assert all(p.returncode == 0 for p in procs), [o[1][-2000:] for o in outs]
+        return json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][-1])
+
+    one, two = run(1, 2 * G), run(2, G)
+    assert two["n_gpus"] == 2 and two["config"]["global_batch"] == 2 * G
+    for k in ("sims", "evals", "games", "positions"):
+        assert two["work"][k] == one["work"][k], (k, one["work"], two["work"])
+    assert two["work"]["games"] == 2 * G
