@@ -66,15 +66,12 @@ constexpr int kLinK = 1536;                // padded to 48 k-steps of 32
 constexpr int kLinKSteps = kLinK / 32;     // 48
 constexpr int kLinPitch = kLinK + 16;      // the largest head-feature pitch (lin_pitch) sizes the overlay
 // The fused linear has 8 outputs (7 logits + the value), so an MFMA B fragment
-// of 16 columns would be half zeros.  SPAI_LIN_HALVES packs the two K halves
-// into the 16 columns instead: column n = (output n & 7, K half n >> 3), A row
-// m = (position m & 7, K half m >> 3), and the diagonal blocks of D are the two
-// halves' partial sums -- 24 k-steps and 24 KiB of staged weights, not 48.
-#ifndef SPAI_LIN_HALVES
-#define SPAI_LIN_HALVES 1
-#endif
-constexpr int kLinHalves = SPAI_LIN_HALVES ? 2 : 1;
-constexpr int kLinBSteps = kLinKSteps / kLinHalves;   // B-fragment k-steps (staged, 1 KiB each)
+// of 16 columns would be half zeros.  The two K halves are packed into the 16
+// columns instead: column n = (output n & 7, K half n >> 3), A row m =
+// (position m & 7, K half m >> 3), and the diagonal blocks of D are the two
+// halves' partial sums -- 24 k-steps and 24 KiB of weights, not 48.
+constexpr int kLinHalves = 2;
+constexpr int kLinBSteps = kLinKSteps / kLinHalves;   // B-fragment k-steps (1 KiB each)
 constexpr int kH = kY;                     // bf16 head features [8][kLinPitch] overlay Y
 constexpr int kHBytes = kP * 128;          // (all of Y)
 constexpr int kB = kH + kHBytes;           // 8 x (mine, theirs)
@@ -87,15 +84,11 @@ constexpr int kPlanes = kBias + kBiasFloats * 4;   // stem neighbour planes [8][
 constexpr int kPlaneRow = 34;
 constexpr int kWStem = kPlanes + kS * kPlaneRow * 8;   // stem weight fragments [4 ct][64 lanes] x 16 B, staged once
 constexpr int kTab = kWStem + 4 * 64 * 16;         // k_geo_init: one S's row-group table [42] x 16 B (NetParams::geo)
-// The fused linear's B fragments: SPAI_LIN_REGS loads each wave's 6 k-steps
-// straight into registers at the head conv's start (no LDS copy); otherwise they
-// are staged in LDS at kLinW by LDS-DMA (stage_linear).
-#ifndef SPAI_LIN_REGS
-#define SPAI_LIN_REGS 1
-#endif
-constexpr int kLinW = kTab + 42 * 16;             // [24 ks][64 lanes] x 16 B (SPAI_LIN_REGS = 0)
+// The fused linear's B fragments: each wave loads its 6 k-steps straight into
+// registers at the head conv's start (an LDS-DMA copy made the compiler wait
+// vmcnt(0) at the head k-loop's first weight use).
 constexpr int kLinWPer = kLinBSteps / kWaves;      // B fragments per wave
-constexpr int kLdsBytes = kLinW + (SPAI_LIN_REGS ? 0 : kLinBSteps * 1024);
+constexpr int kLdsBytes = kTab + 42 * 16;
 constexpr int kStamps = 24;                // phase stamps per wave in the diagnostic mode (17..19: inside block 0 conv1;
                                            // 20/21: s_memtime / s_memrealtime at kernel entry, 22: s_memrealtime at the
                                            // first group's stamp 0, 23: s_memrealtime after the last group)
@@ -494,7 +487,13 @@ __device__ __forceinline__ void final_tap_epilogue(uint8_t *smem, const Geo<Plan
     static_assert(CT == 4, "fused epilogue: 64-channel layers");
     auto live = [](int t, int ks) { return !((tap_skip(S, PL::gpt(t)) >> (ks >> 1)) & 1); };
     auto task_on = [](int i) { return !(EPI == 3 && PL::co(i) == 3); };   // the head has no co tile 3
-    uint4 id[2];   // residual identities (residual_mfma)
+    // Residual add as one more MFMA per task: acc += I * x, B = the center-tap
+    // fragment of the 32-channel block that holds the task's co tile (read from
+    // OUT, which still holds the block input x), A = an identity selecting its 16
+    // channels.  One exact product 1 * x plus zero products and a single fp32
+    // rounding: the value of the VALU add it replaces, for 8 issue cycles per task
+    // instead of ~8 VALU instructions.
+    uint4 id[2];   // the residual identities
     uint4 rb[3];   // residual B fragments, two tasks ahead
     if (EPI == 2) {
         const int m = lane & 15, q = lane >> 4;
@@ -570,12 +569,9 @@ __device__ __forceinline__ void final_tap_epilogue(uint8_t *smem, const Geo<Plan
     }
 }
 
-#ifndef SPAI_FUSE_EPI
-#define SPAI_FUSE_EPI 1
-#endif
 // EPI > 0 fuses the layer's epilogue into its last tap (k-steps 16 and 17): the
 // final tap runs task-major -- each task's two MFMAs back to back (EPI = 2: plus
-// the residual MFMA, see residual_mfma), and the ReLU/bf16 pack and LDS store of
+// the residual MFMA of final_tap_epilogue), and the ReLU/bf16 pack and LDS store of
 // task i - 2 ride in the MFMA gaps of task i instead of a serial epilogue after
 // the k-loop.  Safe to store while other waves still run this layer: OUT is not
 // this layer's input, and a residual read that meets another wave's fresh store
@@ -691,67 +687,16 @@ __device__ __forceinline__ void load_a_first(const uint4 *__restrict__ w, int la
         for (int c = 0; c < CTL; ++c) A[k][c] = w[(k * CT + C0 + c) * 64 + lane];
 }
 
-// epilogue for a 64-channel bf16 output: relu(acc [+ residual]) -> LDS at OUT.
-// The residual reads are all issued before the first use so their LDS latency
-// is paid once, not once per tile.
-template <int W, int NPT, int OUT, bool RESIDUAL>
+// epilogue for a 64-channel bf16 output: relu(acc) -> LDS at OUT (the stem's;
+// the trunk and head convs fuse theirs into the last tap, final_tap_epilogue)
+template <int W, int NPT, int OUT>
 __device__ __forceinline__ void epilogue_act(uint8_t *smem, const Geo<Plan<W, 4, NPT>::NT> &g, f32x4 (&acc)[Plan<W, 4, NPT>::n]) {
     using PL = Plan<W, 4, NPT>;
-#ifdef SPAI_EXP_NO_EPI
-    if (acc[0][0] != 12345.f) return;
-#endif
-    uint2 r[RESIDUAL ? PL::n : 1];
-    if (RESIDUAL) {
-#pragma unroll
-        for (int i = 0; i < PL::n; ++i) r[i] = *(const uint2 *)(smem + OUT + (g.epi[PL::pt(i)] ^ (PL::co(i) << 5)));
-    }
 #pragma unroll
     for (int i = 0; i < PL::n; ++i) {
         const int off = OUT + (g.epi[PL::pt(i)] ^ (PL::co(i) << 5));
-        float v0 = acc[i][0], v1 = acc[i][1], v2 = acc[i][2], v3 = acc[i][3];
-        if (RESIDUAL) {
-            v0 += __builtin_bit_cast(float, r[i].x << 16);
-            v1 += __builtin_bit_cast(float, r[i].x & 0xFFFF0000u);
-            v2 += __builtin_bit_cast(float, r[i].y << 16);
-            v3 += __builtin_bit_cast(float, r[i].y & 0xFFFF0000u);
-        }
-        *(uint2 *)(smem + off) = make_uint2(pack_relu_bf16x2(v0, v1), pack_relu_bf16x2(v2, v3));
+        *(uint2 *)(smem + off) = make_uint2(pack_relu_bf16x2(acc[i][0], acc[i][1]), pack_relu_bf16x2(acc[i][2], acc[i][3]));
     }
-}
-
-// Residual add as one more MFMA per task: acc += I * x, B = the center-tap
-// fragment of the 32-channel block that holds the task's co tile (read from the
-// conv's output buffer, which still holds x), A = an identity selecting those 16
-// channels.  One exact product 1 * x plus zero products and a single fp32
-// rounding: the same value as the VALU add it replaces, for 8 issue cycles per
-// task instead of ~8 VALU instructions.  Another wave may be storing the other
-// 16 channels of the block meanwhile (co-major split); those lanes of B meet
-// zeros in A and the values are finite bf16 either way.
-#ifndef SPAI_RES_MFMA
-#define SPAI_RES_MFMA 1
-#endif
-template <int W, int NPT, int OUT>
-__device__ __forceinline__ void residual_mfma(const uint8_t *smem, const Geo<Plan<W, 4, NPT>::NT> &g, int lane,
-                                              f32x4 (&acc)[Plan<W, 4, NPT>::n]) {
-    using PL = Plan<W, 4, NPT>;
-    const int m = lane & 15, q = lane >> 4;
-    uint4 id[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int j = 16 * h + m - 8 * q;   // this lane's k slot that holds the 1, if any
-        uint32_t w[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) w[e] = j == 2 * e ? 0x3F80u : j == 2 * e + 1 ? 0x3F800000u : 0u;
-        id[h] = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    uint4 b[PL::n];
-#pragma unroll
-    for (int i = 0; i < PL::n; ++i)
-        b[i] = *(const uint4 *)(smem + (OUT - 256) + (g.b(PL::pt(i), 4) ^ ((PL::co(i) >> 1) << 6)));
-#pragma unroll
-    for (int i = 0; i < PL::n; ++i)
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(id[PL::co(i) & 1]), as_bf16x8(b[i]), acc[i], 0, 0,
-                                                        0);
 }
 
 // stem: one k-step, k = tap*3 + plane (27 of 32 used).  Bitboard path: the
@@ -814,25 +759,7 @@ __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const fl
     for (int i = 0; i < PL::n; ++i)
         acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[PL::co(i)]), as_bf16x8(bv[PL::pt(i)]),
                                                         b4[PL::co(i)], 0, 0, 0);
-    epilogue_act<W, NPT, kX, false>(smem, g, acc);
-}
-
-// The fused linear's weights into LDS (kLinW): wave W copies k-steps
-// [12W, 12W+12) with global_load_lds (1 KiB per instruction, no VGPRs).  Issued
-// at the head conv's start: while such a copy is in flight the compiler waits
-// for every outstanding vector load at the next use of a register load, and the
-// head's first register-loaded weights are used DA-1 k-steps later (its first
-// fragments were prefetched by the last residual conv), by which time the copy
-// has landed.  torso_and_heads waits for it (vmcnt(0) + the head's barrier)
-// before the linear reads it.
-template <int W>
-__device__ __forceinline__ void stage_linear(uint8_t *smem, const NetParams &P, int lane) {
-#pragma unroll
-    for (int i = 0; i < kLinBSteps / kWaves; ++i) {
-        const int ks = W * (kLinBSteps / kWaves) + i;
-        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1))) *)(P.w_lin + ks * 64 + lane),
-                                         (void __attribute__((address_space(3))) *)(smem + kLinW + ks * 1024), 16, 0, 0);
-    }
+    epilogue_act<W, NPT, kX>(smem, g, acc);
 }
 
 // The head conv (64 -> 32 policy + 3 value channels) on the 64-channel layers'
@@ -853,12 +780,8 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
         const int s = aux[t] & 255, b = aux[t] >> 8;   // b = col*7 + row
         hoff[t] = s < S ? s * lin_pitch(S) + ((b % c4::kCols) * c4::kCols + b / c4::kCols) * kHC : -1;
     }
-    if (SPAI_LIN_REGS) {   // this wave's linear B fragments, consumed after the head conv
 #pragma unroll
-        for (int i = 0; i < kLinWPer; ++i) wlin[i] = P.w_lin[(W * kLinWPer + i) * 64 + lane];
-    } else {
-        stage_linear<W>(smem, P, lane);
-    }
+    for (int i = 0; i < kLinWPer; ++i) wlin[i] = P.w_lin[(W * kLinWPer + i) * 64 + lane];   // consumed after the head conv
     f32x4 acc[PL::n];
     conv_mfma<W, 4, NPT, S, kX, DA, b_depth(S), 3, kH>(smem, g, (const float *)(smem + kBias) + kHid * (1 + 2 * P.blocks),
                                                       P.w_head, P.w_head, lane, A, acc, hoff);
@@ -879,33 +802,29 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
 
 // fused policy|value linear on MFMA: out[s][o] = sum_k H[s][k] * Wl[o][k]
 // (o < 7 policy logits over k < 1344, o = 7 value pre-activation over
-// 1344 <= k < 1470; connect_four.rs:63-64,69-70).  Wave W takes k-steps
-// [12W, 12W+12) of 48 (B fragments from LDS, stage_linear); partial sums go to LDS.
+// 1344 <= k < 1470; connect_four.rs:63-64,69-70), the two K halves packed into
+// one 16-column B fragment (kLinHalves).  Wave W takes B k-steps [6W, 6W+6) of
+// 24, their fragments held in registers (wlin); partial sums go to LDS.
 template <int W, int S>
 __device__ __forceinline__ void linear_mfma(uint8_t *smem, int lane, const uint4 (&wlin)[kLinWPer]) {
     constexpr int k0 = (kLinBSteps / kWaves) * W, k1 = k0 + kLinBSteps / kWaves;
     const int m = lane & 15, q = lane >> 4;
-    // A row m: position m & 7 over K half m >> 3 (SPAI_LIN_HALVES), else position m
-    const int s = SPAI_LIN_HALVES ? (m & 7) : m, kh = SPAI_LIN_HALVES ? (m >> 3) : 0;
+    // A row m: position m & 7 over K half m >> 3
+    const int s = m & 7, kh = m >> 3;
     const uint8_t *hrow = s < S ? smem + kH + (s * lin_pitch(S) + kh * (kLinK / 2)) * 2 + q * 16 : smem + kZ + q * 16;
     const int hstep = s < S ? 64 : 0;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = k0; ks < k1; ++ks) {
         const uint4 a = *(const uint4 *)(hrow + ks * hstep);
-        const uint4 b = SPAI_LIN_REGS ? wlin[ks - k0] : *(const uint4 *)(smem + kLinW + ks * 1024 + lane * 16);
+        const uint4 b = wlin[ks - k0];
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a), as_bf16x8(b), acc, 0, 0, 0);
     }
     // D[row 4q + r][col n = lane & 15]
     float *L = (float *)(smem + kL) + W * kLinHalves * 64;
-    if (SPAI_LIN_HALVES) {   // keep the diagonal blocks: row half (q >> 1) == column half (n >> 3)
-        if ((q >> 1) == (m >> 3)) {
+    if ((q >> 1) == (m >> 3)) {   // keep the diagonal blocks: row half (q >> 1) == column half (n >> 3)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) L[(q >> 1) * 64 + (4 * (q & 1) + r) * 8 + (m & 7)] = acc[r];
-        }
-    } else if (q < 2 && m < 8) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) L[(4 * q + r) * 8 + m] = acc[r];
+        for (int r = 0; r < 4; ++r) L[(q >> 1) * 64 + (4 * (q & 1) + r) * 8 + (m & 7)] = acc[r];
     }
 }
 
@@ -929,7 +848,7 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
     for (int b = 0; b < P.blocks; ++b) {   // relu(x + BN(conv(relu(BN(conv(x)))))), model/mod.rs:152-165
         f32x4 acc[Plan<W, 4, NPT>::n];
         const int l1 = 2 * b, l2 = 2 * b + 1;
-        conv_mfma<W, 4, NPT, S, kX, DA, DB, SPAI_FUSE_EPI ? 1 : 0, kY>(smem, g, bias + kHid * (1 + l1), P.w_res + l1 * kLayer,
+        conv_mfma<W, 4, NPT, S, kX, DA, DB, 1, kY>(smem, g, bias + kHid * (1 + l1), P.w_res + l1 * kLayer,
                                                                     P.w_res + l2 * kLayer, lane, A, acc, aux);
 #ifdef SPAI_DIAG
         if (b == 0 && !kDiagHead) {   // make the k-loop's results visible before the stamp
@@ -937,7 +856,6 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
             stamp(P, W, lane, 17);
         }
 #endif
-        if (!SPAI_FUSE_EPI) epilogue_act<W, NPT, kY, false>(smem, g, acc);
 #ifdef SPAI_DIAG
         if (b == 0 && !kDiagHead) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -949,22 +867,14 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
         if (b == 0 && !kDiagHead) stamp(P, W, lane, 19);
 #endif
         if (l1 < 12) stamp(P, W, lane, 2 + l1);
-        conv_mfma<W, 4, NPT, S, kY, DA, DB, SPAI_FUSE_EPI ? 2 : 0, kX>(smem, g, bias + kHid * (1 + l2), P.w_res + l2 * kLayer,
+        conv_mfma<W, 4, NPT, S, kY, DA, DB, 2, kX>(smem, g, bias + kHid * (1 + l2), P.w_res + l2 * kLayer,
                             b + 1 < P.blocks ? P.w_res + (l2 + 1) * kLayer : P.w_head, lane, A, acc, aux);
-        if (SPAI_FUSE_EPI) {
-        } else if (SPAI_RES_MFMA) {
-            residual_mfma<W, NPT, kX>(smem, g, lane, acc);
-            epilogue_act<W, NPT, kX, false>(smem, g, acc);
-        } else {
-            epilogue_act<W, NPT, kX, true>(smem, g, acc);
-        }
         layer_barrier();
         if (l2 < 12) stamp(P, W, lane, 2 + l2);
     }
     if (kDiagHead) stamp(P, W, lane, 19);   // diagnostic head mode: 19 = before the head, 17 = head k-loop, 18 = H written
     uint4 wlin[kLinWPer];
     head_layer<W, S, DA>(smem, P, lane, g, aux, A, wlin);
-    if (!SPAI_LIN_REGS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stage_linear copies have landed
     __syncthreads();
     stamp(P, W, lane, 14);
     linear_mfma<W, S>(smem, lane, wlin);
@@ -1294,16 +1204,16 @@ int net_create(spai_engine *e, int blocks, int hidden, const float *params, size
     }
     up(n->w_head, wh);
     up(n->b_head, bh);
-    // fused linear as MFMA B fragments: [ks 48][lane 64][8], lane -> o = lane & 15,
-    // k = ks*32 + 8*(lane>>4) + j over the head features H[s][cell*36 + c]; the
-    // reference flattens c*42 + cell (policy c < 32 -> logits 0..6, value c = 32..34 -> o = 7)
-    // (SPAI_LIN_HALVES: [ks 24][lane 64][8], o = lane & 7, k = (lane >> 3 & 1) * 768 + ks*32 + ...)
+    // fused linear as MFMA B fragments with the K halves packed: [ks 24][lane 64][8],
+    // lane -> o = lane & 7, k = (lane >> 3 & 1) * 768 + ks*32 + 8*(lane >> 4) + j over
+    // the head features H[s][cell*36 + c]; the reference flattens c*42 + cell
+    // (policy c < 32 -> logits 0..6, value c = 32..34 -> o = 7)
     std::vector<uint16_t> wlin((size_t)kLinBSteps * 64 * 8, 0);
     for (int ks = 0; ks < kLinBSteps; ++ks)
         for (int l = 0; l < 64; ++l)
             for (int j = 0; j < 8; ++j) {
-                const int o = SPAI_LIN_HALVES ? (l & 7) : (l & 15);
-                const int k = (SPAI_LIN_HALVES ? ((l >> 3) & 1) * (kLinK / 2) : 0) + ks * 32 + 8 * (l >> 4) + j;
+                const int o = l & 7;
+                const int k = ((l >> 3) & 1) * (kLinK / 2) + ks * 32 + 8 * (l >> 4) + j;
                 const int cell = k / kHC, c = k % kHC;
                 float v = 0.f;
                 if (k < kLinFeat && o < 7 && c < 32) v = pol_w[(size_t)o * kPolIn + c * c4::kCells + cell];
