@@ -79,6 +79,7 @@ constexpr int kL = kB + kS * 16;           // linear partials [4 waves][halves][
 constexpr int kMaxBlocks = 20;
 constexpr int kBiasFloats = kHid + 2 * kMaxBlocks * kHid + kHid;   // stem, residual convs, head (64 padded)
 constexpr int kBias = kL + kWaves * kLinHalves * 64 * 4; // all conv biases, staged once per workgroup
+constexpr int kBiasPer = (kBiasFloats + kThreads - 1) / kThreads;   // per thread
 constexpr int kPlanes = kBias + kBiasFloats * 4;   // stem neighbour planes [8][34] u64 (272-B rows: positions
                                                    // in different 16-B bank groups)
 constexpr int kPlaneRow = 34;
@@ -99,9 +100,7 @@ struct NetParams {
     const uint4 *w_stem;   // [4 ct][64 lanes] 16 B fragments
     const uint4 *w_res;    // [2*blocks][18 ks][4 ct][64]
     const uint4 *w_head;   // [18][4][64]: a 64-channel layer whose co tile 3 is never computed
-    const float *b_stem;   // [64]
-    const float *b_res;    // [2*blocks][64]
-    const float *b_head;   // [64]
+    const float *b_conv;   // conv biases, BN folded: [64 stem | 2*blocks x 64 residual convs | 64 head conv]
     const uint4 *w_lin;    // [48 ks][64] B fragments of the fused policy|value linear
     const float *b_pol;    // [7]
     const float *b_val;    // [1]
@@ -900,16 +899,6 @@ __device__ __forceinline__ void run_groups(uint8_t *smem, const NetParams &P, ui
                                            float *__restrict__ value, float *__restrict__ logits, int tid) {
     constexpr int wave = W;
     const int lane = tid & 63;
-    // launch constants: the zero blocks, stem weights and every conv bias
-    if (tid < 64) ((uint32_t *)(smem + kZ))[tid] = 0u;
-    else if (tid < 128) ((uint32_t *)(smem + kZ1))[tid - 64] = 0u;
-    ((uint4 *)(smem + kWStem))[tid] = P.w_stem[tid];   // 256 x 16 B
-    {
-        float *bias = (float *)(smem + kBias);
-        const int nres = 2 * P.blocks * kHid;
-        for (int i = tid; i < kHid + nres + kHid; i += kThreads)
-            bias[i] = i < kHid ? P.b_stem[i] : i < kHid + nres ? P.b_res[i - kHid] : P.b_head[i - kHid - nres];
-    }
     for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
         // hide the lane id from loop-invariant code motion: the trunk geometry (and
         // every layer's per-lane addressing) hoisted out of the loop would stay live
@@ -1022,11 +1011,25 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
     __shared__ __attribute__((aligned(16))) uint8_t smem[kLdsBytes];
     stamp(P, threadIdx.x >> 6, threadIdx.x & 63, 20);
     stamp_real(P, threadIdx.x >> 6, threadIdx.x & 63, 21);
+    const int tid = threadIdx.x;
+    // launch constants (stem weights, every conv bias): their loads are issued
+    // together, beside the leaf count's, and land in LDS before the group loop
+    // (staged inside it they were two more dependent round trips per launch)
+    const uint4 ws = P.w_stem[tid];   // 256 x 16 B
+    const int nbias = (2 * P.blocks + 2) * kHid;
+    float bv[kBiasPer];
+#pragma unroll
+    for (int j = 0; j < kBiasPer; ++j) bv[j] = tid + j * kThreads < nbias ? P.b_conv[tid + j * kThreads] : 0.f;
     const uint32_t count = count_ptr ? *count_ptr : count_imm;
     const int S = force_s > 0 ? force_s : group_size(count, gridDim.x);
     const int ngroups = (int)((count + S - 1) / S);
     if ((int)blockIdx.x >= ngroups) return;
-    const int tid = threadIdx.x;
+    if (tid < 64) ((uint32_t *)(smem + kZ))[tid] = 0u;   // the zero blocks below X and Y
+    else if (tid < 128) ((uint32_t *)(smem + kZ1))[tid - 64] = 0u;
+    ((uint4 *)(smem + kWStem))[tid] = ws;
+#pragma unroll
+    for (int j = 0; j < kBiasPer; ++j)
+        if (tid + j * kThreads < nbias) ((float *)(smem + kBias))[tid + j * kThreads] = bv[j];
 #ifdef SPAI_FWD_PRIO
     __builtin_amdgcn_s_setprio(SPAI_FWD_PRIO);   // experiment: issue priority against co-resident tree kernels
 #endif
@@ -1197,13 +1200,14 @@ int net_create(spai_engine *e, int blocks, int hidden, const float *params, size
         }
     };
     up(n->w_stem, ws);
-    up(n->b_stem, bs);
-    if (blocks > 0) {
-        up(n->w_res, wr);
-        up(n->b_res, br);
-    }
+    if (blocks > 0) up(n->w_res, wr);
     up(n->w_head, wh);
-    up(n->b_head, bh);
+    {
+        std::vector<float> bc(bs);
+        bc.insert(bc.end(), br.begin(), br.end());
+        bc.insert(bc.end(), bh.begin(), bh.end());
+        up(n->b_conv, bc);
+    }
     // fused linear as MFMA B fragments with the K halves packed: [ks 24][lane 64][8],
     // lane -> o = lane & 7, k = (lane >> 3 & 1) * 768 + ks*32 + 8*(lane >> 4) + j over
     // the head features H[s][cell*36 + c]; the reference flattens c*42 + cell
@@ -1260,7 +1264,7 @@ int net_create(spai_engine *e, int blocks, int hidden, const float *params, size
 void net_destroy(spai_net *n) {
     if (!n) return;
     for (auto *b : {&n->w_stem, &n->w_res, &n->w_head, &n->w_lin}) b->release();
-    for (auto *b : {&n->b_stem, &n->b_res, &n->b_head, &n->b_pol, &n->b_val, &n->f32, &n->io_x,
+    for (auto *b : {&n->b_conv, &n->b_pol, &n->b_val, &n->f32, &n->io_x,
                     &n->io_logits, &n->io_value, &n->io_priors})
         b->release();
     n->io_mine.release();
@@ -1276,9 +1280,7 @@ static NetParams params_of(const spai_net *n) {
     P.w_stem = (const uint4 *)n->w_stem.p;
     P.w_res = (const uint4 *)n->w_res.p;
     P.w_head = (const uint4 *)n->w_head.p;
-    P.b_stem = n->b_stem.p;
-    P.b_res = n->b_res.p;
-    P.b_head = n->b_head.p;
+    P.b_conv = n->b_conv.p;
     P.w_lin = (const uint4 *)n->w_lin.p;
     P.b_pol = n->b_pol.p;
     P.b_val = n->b_val.p;

