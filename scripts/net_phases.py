@@ -25,6 +25,9 @@ for S in range(1, 9):
           f"block0 conv1: k-loop {c[17] - c[1]:.0f}, epilogue {c[18] - c[17]:.0f}, barrier {c[19] - c[18]:.0f}; "
           f"wall: entry->group {c[21] / 1e3:.2f} us ({c[20]:.0f} cyc), group {c[22] / 1e3:.2f} us, "
           f"launch span {c[23] / 1e3:.2f} us, clock {c[16] / max(c[22], 1):.2f} GHz")
+    if os.environ.get("SPAI_PRINT_ENTRY"):   # diagnostic build with -DSPAI_DIAG_ENTRY
+        print(f"    entry (shader cycles): constants in LDS {c[20] + c[17]:.0f}, geometry + bitboards loaded "
+              f"{c[20] + c[18]:.0f}, planes stored {c[20] + c[19]:.0f}, group start {c[20]:.0f}")
 os.environ.pop("SPAI_PHASE_S")
 net.close()
 e.close()

@@ -182,6 +182,7 @@ int spai_engine_destroy(spai_engine *e) {
         B.priors.release();
         B.value.release();
         B.iter_counts.release();
+        B.iter_more.release();
     }
     e->games.x.release();
     e->games.o.release();

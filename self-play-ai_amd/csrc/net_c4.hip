@@ -120,6 +120,14 @@ constexpr bool kDiagHead = true;   // stamps 17..19 time the head instead of blo
 #else
 constexpr bool kDiagHead = false;
 #endif
+// SPAI_DIAG_ENTRY (diagnostic builds): stamps 17..19 time the launch prologue
+// instead -- 17 constants in LDS, 18 first group's geometry and bitboards loaded,
+// 19 its planes stored (each behind a full wait, so the phases are serialised)
+#ifdef SPAI_DIAG_ENTRY
+constexpr bool kDiagEntry = true;
+#else
+[[maybe_unused]] constexpr bool kDiagEntry = false;
+#endif
 __device__ __forceinline__ void stamp(const NetParams &P, int wave, int lane, int k) {
 #ifdef SPAI_DIAG
     if (P.stamps && lane == 0) P.stamps[((size_t)blockIdx.x * kWaves + wave) * kStamps + k] = __builtin_amdgcn_s_memtime();
@@ -850,20 +858,20 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
         conv_mfma<W, 4, NPT, S, kX, DA, DB, 1, kY>(smem, g, bias + kHid * (1 + l1), P.w_res + l1 * kLayer,
                                                                     P.w_res + l2 * kLayer, lane, A, acc, aux);
 #ifdef SPAI_DIAG
-        if (b == 0 && !kDiagHead) {   // make the k-loop's results visible before the stamp
+        if (b == 0 && !kDiagHead && !kDiagEntry) {   // make the k-loop's results visible before the stamp
             asm volatile("" ::"v"(acc[0][0]), "v"(acc[PL4::n - 1][3]));
             stamp(P, W, lane, 17);
         }
 #endif
 #ifdef SPAI_DIAG
-        if (b == 0 && !kDiagHead) {
+        if (b == 0 && !kDiagHead && !kDiagEntry) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             stamp(P, W, lane, 18);
         }
 #endif
         layer_barrier();
 #ifdef SPAI_DIAG
-        if (b == 0 && !kDiagHead) stamp(P, W, lane, 19);
+        if (b == 0 && !kDiagHead && !kDiagEntry) stamp(P, W, lane, 19);
 #endif
         if (l1 < 12) stamp(P, W, lane, 2 + l1);
         conv_mfma<W, 4, NPT, S, kY, DA, DB, 2, kX>(smem, g, bias + kHid * (1 + l2), P.w_res + l2 * kLayer,
@@ -921,6 +929,12 @@ __device__ __forceinline__ void run_groups(uint8_t *smem, const NetParams &P, ui
             ((uint64_t *)(smem + kB))[2 * tid] = m;
             ((uint64_t *)(smem + kB))[2 * tid + 1] = t;
         }
+#ifdef SPAI_DIAG_ENTRY
+        if (grp == (int)blockIdx.x) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            stamp(P, wave, lane, 18);
+        }
+#endif
         if (!FROM_X) {   // neighbour planes N[s][k]: k = tap*3 + plane, shifted so bit b = value at b's neighbour
             const int s = tid >> 5, k = tid & 31;
             uint64_t v = 0;
@@ -933,6 +947,12 @@ __device__ __forceinline__ void run_groups(uint8_t *smem, const NetParams &P, ui
             }
             ((uint64_t *)(smem + kPlanes))[s * kPlaneRow + k] = v;
         }
+#ifdef SPAI_DIAG_ENTRY
+        if (grp == (int)blockIdx.x) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            stamp(P, wave, lane, 19);
+        }
+#endif
         __syncthreads();
         stamp(P, wave, lane, 0);
         if (grp == (int)blockIdx.x) stamp_real(P, wave, lane, 22);
@@ -1030,6 +1050,10 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
 #pragma unroll
     for (int j = 0; j < kBiasPer; ++j)
         if (tid + j * kThreads < nbias) ((float *)(smem + kBias))[tid + j * kThreads] = bv[j];
+#ifdef SPAI_DIAG_ENTRY
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    stamp(P, tid >> 6, tid & 63, 17);
+#endif
 #ifdef SPAI_FWD_PRIO
     __builtin_amdgcn_s_setprio(SPAI_FWD_PRIO);   // experiment: issue priority against co-resident tree kernels
 #endif
@@ -1397,7 +1421,7 @@ int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
         for (int w = 0; w < kWaves; ++w) {
             const unsigned long long *sp = hs.data() + ((size_t)g * kWaves + w) * kStamps;
             if (!sp[0] || !sp[16]) continue;   // (a workgroup with no group)
-            for (int k = 0; k < 20; ++k) cycles[k] += sp[k] ? (double)(sp[k] - sp[0]) : 0.0;
+            for (int k = 0; k < 20; ++k) cycles[k] += sp[k] ? (double)(long long)(sp[k] - sp[0]) : 0.0;
             cycles[20] += (double)(sp[0] - sp[20]);   // (the last group's stamp 0: one group per workgroup in the sweeps)
             cycles[21] += 10.0 * (double)(sp[22] - sp[21]);
             cycles[22] += 10.0 * (double)(sp[23] - sp[22]);

@@ -5,7 +5,7 @@
 // One search iteration (mcts.rs:214-285) is two launches per search chain:
 //   evaluate        the fused ResNet forward (net_c4.hip) or a stub evaluator
 //                   over this iteration's leaf batch;
-//   k_expand_select per tree, 8 lanes (one per child slot): expand the tree's
+//   k_expand_select per tree, 8 lanes (one per board column): expand the tree's
 //                   leaf of this iteration if it had one (legal moves by
 //                   ballot, children packed by a prefix count, priors written,
 //                   value backed up along the recorded path, lanes splitting
@@ -53,11 +53,13 @@ struct TreeView {
     uint8_t *depth;
     uint32_t *slot;   // the tree's leaf slot in the current batch, kNoSlot if terminal
     uint32_t *left;   // tail run-on mode: search iterations the tree still has to run
+    uint32_t *evals;  // live leaves of this search call (the tail-mode policy's input)
 };
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
 struct BatchView {
     uint32_t *count;
+    uint32_t *more;   // tail mode: set when a tree stopped at the run cap with iterations left (else null)
     uint32_t *tree;
     uint64_t *mine, *theirs;
     float *priors;
@@ -90,11 +92,13 @@ __device__ __forceinline__ float ucb(float sqrt_np, const uint4 &ch, float c) {
 constexpr int kLevelsPerLane = kMaxDepth / kLanesPerTree;
 // (The loads are unconditional -- levels past d read the path's root, whose node
 // exists -- so that no branch separates them: hipcc waits vmcnt(0) at each one.)
-__device__ __forceinline__ void backup_nodes(uint4 *nodes, const uint32_t (&node)[kLevelsPerLane], int d, float v,
-                                             int lane8) {
-    uint2 r[kLevelsPerLane];
+__device__ __forceinline__ void backup_load(const uint4 *nodes, const uint32_t (&node)[kLevelsPerLane], int d,
+                                            int lane8, uint2 (&r)[kLevelsPerLane]) {
 #pragma unroll
     for (int j = 0; j < kLevelsPerLane; ++j) r[j] = *(const uint2 *)(nodes + (lane8 + 8 * j <= d ? node[j] : node[0]));
+}
+__device__ __forceinline__ void backup_store(uint4 *nodes, const uint32_t (&node)[kLevelsPerLane], int d, float v,
+                                             int lane8, const uint2 (&r)[kLevelsPerLane]) {
 #pragma unroll
     for (int j = 0; j < kLevelsPerLane; ++j) {
         const int lvl = lane8 + 8 * j;
@@ -104,13 +108,11 @@ __device__ __forceinline__ void backup_nodes(uint4 *nodes, const uint32_t (&node
         }
     }
 }
-
-// the same from the path recorded in memory (expand: the select was an earlier launch)
-__device__ __forceinline__ void backup(uint4 *nodes, const uint32_t *path, int d, float v, int lane8) {
-    uint32_t node[kLevelsPerLane];
-#pragma unroll
-    for (int j = 0; j < kLevelsPerLane; ++j) node[j] = path[lane8 + 8 * j <= d ? lane8 + 8 * j : 0];
-    backup_nodes(nodes, node, d, v, lane8);
+__device__ __forceinline__ void backup_nodes(uint4 *nodes, const uint32_t (&node)[kLevelsPerLane], int d, float v,
+                                             int lane8) {
+    uint2 r[kLevelsPerLane];
+    backup_load(nodes, node, d, lane8, r);
+    backup_store(nodes, node, d, v, lane8, r);
 }
 
 // this lane's bit of its tree's 8-lane group in a wave-wide ballot
@@ -153,14 +155,20 @@ __device__ __forceinline__ void cand_step(Cand &c) {
     c.w = take ? o.w : c.w;
 }
 
-// a tree's root for this search call: node id and position (constant while it runs)
+// a tree's root for this search call: node id and position (constant while it
+// runs), and its record's visit count and children word, kept current in
+// registers (each iteration's backup adds one visit; an expansion of the root
+// sets its children), so a descent starts without reloading it
 struct RootInfo {
     uint32_t node;
     uint64_t x, o;
     uint8_t n, status;
+    uint32_t rn, rw;
 };
 __device__ __forceinline__ RootInfo load_root(const TreeView &T, uint32_t t) {
-    return RootInfo{T.root[t], T.root_x[t], T.root_o[t], T.root_n[t], T.root_status[t]};
+    const uint32_t node = T.root[t];
+    const uint4 r = T.nodes[(size_t)t * T.cap + node];
+    return RootInfo{node, T.root_x[t], T.root_o[t], T.root_n[t], T.root_status[t], r.x, r.w};
 }
 
 // One PUCT descent of tree t (mcts.rs:235-250) by its 8 lanes.  A terminal leaf
@@ -185,8 +193,7 @@ __device__ __forceinline__ Descent descend(const TreeView &T, uint32_t t, const 
     o = root.o;
     n = root.n;
     uint8_t status = root.status;
-    const uint4 r0 = nodes[node];
-    uint32_t rn = r0.x, rw = r0.w;   // the current node's visit count and children word
+    uint32_t rn = root.rn, rw = root.rw;   // the current node's visit count and children word
     // path levels == lane8 (mod 8) kept in this lane's registers (kMaxDepth = 6 x 8)
     uint32_t pr[kLevelsPerLane] = {node, 0u, 0u, 0u, 0u, 0u};
     const int top = 7 * lane8 + 5;   // this column's top cell (lane 7: none)
@@ -247,6 +254,7 @@ __device__ __forceinline__ void slot_leaf(const TreeView &T, const BatchView &B,
                                           uint64_t o, uint8_t n) {
     if (lane8 == 0) {
         const uint32_t slot = atomicAdd(B.count, 1u);
+        __hip_atomic_fetch_add(T.evals + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // result unused: no wait
         const bool xm = c4::x_to_move(n);
         T.slot[t] = slot;
         B.tree[slot] = t;
@@ -261,13 +269,14 @@ __device__ __forceinline__ void slot_leaf(const TreeView &T, const BatchView &B,
 // RUN_ON (tail mode, search()): the tree runs its remaining iterations (T.left)
 // in this launch for as long as they end on terminal leaves -- each is backed
 // up, then the next descent starts -- and stops at the first live leaf, which
-// goes to the batch.  The tree's iterations keep the reference's order (select,
-// backprop, select, ...), so the results equal one descent per launch; a launch
-// then lasts as long as its longest terminal run, which pays off only late in a
-// game, where most iterations need no evaluation.
+// goes to the batch, or after run_cap descents (B.more set: the next pass goes
+// on).  The tree's iterations keep the reference's order (select, backprop,
+// select, ...), so the results equal one descent per launch.  The cap keeps a
+// pass from lasting a solved tree's whole run while a tree that still evaluates
+// waits for the next one.
 template <bool RUN_ON>
-__device__ __forceinline__ void select_tree(const TreeView &T, const BatchView &B, uint32_t t, const RootInfo &root,
-                                            int lane8, float c, uint32_t *err) {
+__device__ __forceinline__ void select_tree(const TreeView &T, const BatchView &B, uint32_t t, RootInfo &root,
+                                            int lane8, float c, uint32_t *err, uint32_t run_cap) {
     if (lane8 == 0) T.slot[t] = kNoSlot;
     uint64_t x, o;
     uint8_t n;
@@ -276,78 +285,104 @@ __device__ __forceinline__ void select_tree(const TreeView &T, const BatchView &
         return;
     }
     uint32_t left = T.left[t];
-    while (left > 0) {
+    for (uint32_t run = 0; left > 0; ++run) {
+        if (run == run_cap) {
+            if (lane8 == 0) atomicOr(B.more, 1u);
+            break;
+        }
         --left;
         const Descent r = descend(T, t, root, lane8, c, err, x, o, n);
         if (r == kLive) slot_leaf(T, B, t, lane8, x, o, n);
         if (r != kTerminal) break;
+        root.rn += 1;   // the backup's visit of the root
         // the next descent reads records the other lanes of this tree just backed
-        // up: same wave, made visible as in k_expand_select
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        // up: one wave, so a wavefront-scope fence (as in k_expand_select)
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     }
     if (lane8 == 0) T.left[t] = left;
 }
 
-// expand leaf slot s of batch B (mcts.rs:116-143) and back its value up (:145-159)
-// Everything the expansion reads is issued together (one memory round trip after
-// the slot): the leaf's depth, every path level this lane backs up (entries past
-// the depth are stale and unused), the leaf position, the arena fill, this lane's
-// prior and the value.  The leaf is path[d], which lane d & 7 already holds.
-__device__ __forceinline__ void expand_leaf(const TreeView &T, const BatchView &B, uint32_t t, uint32_t s, int lane8,
-                                            uint32_t *err) {
-    uint4 *nodes = T.nodes + (size_t)t * T.cap;
+// What an expansion needs of the tree itself (not of its leaf): loaded with the
+// tree's slot, before the slot is known to hold a leaf.
+struct LeafPath {
+    int d;                                 // the leaf's depth
+    uint32_t lv[kLevelsPerLane];           // this lane's path levels (stale past the depth)
+    uint32_t first;                        // the arena fill: the new children's first id
+};
+__device__ __forceinline__ LeafPath load_leaf_path(const TreeView &T, uint32_t t, int lane8) {
+    LeafPath L;
     const uint32_t *path = T.path + (size_t)t * kMaxDepth;
-    const int d = T.depth[t];
-    uint32_t lv[kLevelsPerLane];
+    L.d = T.depth[t];
 #pragma unroll
-    for (int j = 0; j < kLevelsPerLane; ++j) lv[j] = path[lane8 + 8 * j];
+    for (int j = 0; j < kLevelsPerLane; ++j) L.lv[j] = path[lane8 + 8 * j];
+    L.first = T.next_free[t];
+    return L;
+}
+
+// expand leaf slot s of batch B (mcts.rs:116-143) and back its value up (:145-159).
+// One memory round trip after the slot: the leaf's position, this lane's prior
+// and the value, together with the records of the path levels this lane backs up
+// (the new children are past the arena fill, never on the path); then only
+// stores.  The leaf is path[d], which lane d & 7 holds.  The root's visit count
+// and children word in `root` are brought up to date.
+__device__ __forceinline__ void expand_leaf(const TreeView &T, const BatchView &B, uint32_t t, uint32_t s, int lane8,
+                                            uint32_t *err, const LeafPath &L, RootInfo &root) {
+    uint4 *nodes = T.nodes + (size_t)t * T.cap;
+    const int d = L.d;
+    uint32_t node[kLevelsPerLane];   // this lane's levels of the path; 0 (a valid dummy) past the depth
+#pragma unroll
+    for (int j = 0; j < kLevelsPerLane; ++j) node[j] = lane8 + 8 * j <= d ? L.lv[j] : 0u;
     const uint64_t occ = B.mine[s] | B.theirs[s];
-    const uint32_t first = T.next_free[t];
     const float prior = B.priors[(size_t)s * kPriorStride + lane8];   // lane 7: the stride's padding
     const float value = B.value[s];
+    uint2 r[kLevelsPerLane];
+    backup_load(nodes, node, d, lane8, r);
     // legal actions of the (live) leaf; children in ascending action order (mcts.rs:116-143)
     const bool legal = lane8 < c4::kActions && !((occ >> (7 * lane8 + 5)) & 1ull);
     const uint32_t grp = group_bits(__ballot(legal));
     const uint32_t nch = c4::popc32(grp);
     const uint32_t idx = c4::popc32(grp & ((1u << lane8) - 1u));
+    const uint32_t first = L.first;
     if (first + nch > T.cap) {
         if (lane8 == 0) atomicOr(err, kErrCapacity);
         return;
     }
     if (legal) nodes[first + idx] = make_uint4(0u, 0u, __float_as_uint(prior), kNoChildren);
     if (lane8 == 0) T.next_free[t] = first + nch;
-    uint32_t node[kLevelsPerLane];   // this lane's levels of the path; 0 (a valid dummy) past the depth
-#pragma unroll
-    for (int j = 0; j < kLevelsPerLane; ++j) node[j] = lane8 + 8 * j <= d ? lv[j] : 0u;
     if (lane8 == (d & 7)) {
         uint32_t leaf = node[0];
 #pragma unroll
         for (int j = 1; j < kLevelsPerLane; ++j) leaf = (d >> 3) == j ? node[j] : leaf;
         nodes[leaf].w = first | (nch << 24);
     }
-    backup_nodes(nodes, node, d, value, lane8);
+    backup_store(nodes, node, d, value, lane8, r);
+    root.rn += 1;
+    if (d == 0) root.rw = first | (nch << 24);
 }
 
 template <bool RUN_ON>
 __global__ __launch_bounds__(kBlock) void k_select(TreeView T, BatchView B, const uint32_t *__restrict__ active,
-                                                   uint32_t n_active, float c, uint32_t *err) {
+                                                   uint32_t n_active, float c, uint32_t *err, uint32_t run_cap) {
     const uint32_t gi = (blockIdx.x * blockDim.x + threadIdx.x) / kLanesPerTree;
 #ifdef SPAI_TREE_PRIO
     __builtin_amdgcn_s_setprio(SPAI_TREE_PRIO);   // experiment: issue priority against the co-resident forward
 #endif
     if (gi >= n_active) return;
     const uint32_t t = active[gi];
-    select_tree<RUN_ON>(T, B, t, load_root(T, t), threadIdx.x & (kLanesPerTree - 1), c, err);
+    RootInfo root = load_root(T, t);
+    select_tree<RUN_ON>(T, B, t, root, threadIdx.x & (kLanesPerTree - 1), c, err, run_cap);
 }
 
 // expand this iteration's leaf of every tree (batch `cur`), then select the next
 // iteration's leaf into batch `nxt`.  A tree's lanes are one group of 8 in one
-// wave: its expand stores are made visible to its own select loads by a
-// workgroup-scope fence (vmcnt(0); the CU's L1 is coherent within a workgroup).
+// wave, so its expand stores are seen by its own select loads in program order:
+// a wavefront-scope fence (no instruction; it keeps the compiler from moving the
+// loads above the stores), not a workgroup-scope one (s_waitcnt vmcnt(0): a
+// store round trip on every iteration's critical path).
 template <bool RUN_ON>
 __global__ __launch_bounds__(kBlock) void k_expand_select(TreeView T, BatchView cur, BatchView nxt,
                                                           const uint32_t *__restrict__ active, uint32_t n_active,
-                                                          float c, uint32_t *err) {
+                                                          float c, uint32_t *err, uint32_t run_cap) {
     const uint32_t gi = (blockIdx.x * blockDim.x + threadIdx.x) / kLanesPerTree;
 #ifdef SPAI_TREE_PRIO
     __builtin_amdgcn_s_setprio(SPAI_TREE_PRIO);
@@ -356,10 +391,21 @@ __global__ __launch_bounds__(kBlock) void k_expand_select(TreeView T, BatchView 
     const int lane8 = threadIdx.x & (kLanesPerTree - 1);
     const uint32_t t = active[gi];
     const uint32_t s = T.slot[t];
-    const RootInfo root = load_root(T, t);   // read-only during the search: loaded with the slot, off the chain
-    if (s != kNoSlot) expand_leaf(T, cur, t, s, lane8, err);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    select_tree<RUN_ON>(T, nxt, t, root, lane8, c, err);
+    RootInfo root = load_root(T, t);                      // loaded with the slot, off the chain
+    const LeafPath L = load_leaf_path(T, t, lane8);       // likewise (unused when the tree has no leaf)
+    // the root's and the path's loads retire here: used first (or, with no leaf,
+    // never) after the expansion's branch, whose join would otherwise make the
+    // compiler wait for the expansion's stores too (in-order vmcnt, merged
+    // conservatively over both paths)
+    asm volatile("" ::"v"(root.rn), "v"(root.rw), "v"((uint32_t)root.x), "v"((uint32_t)(root.x >> 32)),
+                 "v"((uint32_t)root.o), "v"((uint32_t)(root.o >> 32)), "v"((uint32_t)root.n), "v"((uint32_t)root.status));
+    asm volatile("" ::"v"(L.d), "v"(L.first), "v"(L.lv[0]), "v"(L.lv[1]), "v"(L.lv[2]), "v"(L.lv[3]), "v"(L.lv[4]),
+                 "v"(L.lv[5]));
+    if (s != kNoSlot) expand_leaf(T, cur, t, s, lane8, err, L, root);
+    // the select reads records this tree's lanes just wrote: lanes of one wave,
+    // whose memory operations are performed in order (no wait for the stores)
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    select_tree<RUN_ON>(T, nxt, t, root, lane8, c, err, run_cap);
 }
 
 // tail mode: every active tree has all `iters` iterations of this search call ahead
@@ -384,14 +430,20 @@ __global__ __launch_bounds__(kBlock) void k_eval_stub(BatchView B, uint32_t max_
 __global__ __launch_bounds__(kBlock) void k_expand(TreeView T, BatchView B, uint32_t max_n, uint32_t *err) {
     const uint32_t s = (blockIdx.x * blockDim.x + threadIdx.x) / kLanesPerTree;
     if (s >= max_n || s >= *B.count) return;
-    expand_leaf(T, B, B.tree[s], s, threadIdx.x & (kLanesPerTree - 1), err);
+    const int lane8 = threadIdx.x & (kLanesPerTree - 1);
+    const uint32_t t = B.tree[s];
+    RootInfo root{};   // (the root's record is not needed after the last expansion)
+    expand_leaf(T, B, t, s, lane8, err, load_leaf_path(T, t, lane8), root);
 }
 
-// per active tree: [0] = root first|nch<<24 (children word), [1..7] child visit counts
-__global__ void k_root_stats(TreeView T, const uint32_t *__restrict__ active, uint32_t n_active, uint32_t *out) {
+// per active tree: [0] = root first|nch<<24 (children word), [1..7] child visit counts;
+// max_evals: the most live leaves one tree evaluated in this search call
+__global__ void k_root_stats(TreeView T, const uint32_t *__restrict__ active, uint32_t n_active, uint32_t *out,
+                             uint32_t *max_evals) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_active) return;
     const uint32_t t = active[i];
+    atomicMax(max_evals, T.evals[t]);
     const uint4 *nodes = T.nodes + (size_t)t * T.cap;
     const uint4 r = nodes[T.root[t]];
     out[i * 8] = r.w;
@@ -410,14 +462,14 @@ __global__ void k_trees_init(TreeView T, uint32_t first_tree, uint32_t n) {
 TreeView tree_view(spai_engine *e) {
     Trees &T = e->trees;
     return TreeView{T.nodes.p, T.cap, T.root.p, T.next_free.p, T.root_x.p, T.root_o.p, T.root_n.p, T.root_status.p,
-                    T.path.p, T.depth.p, T.slot.p, T.left.p};
+                    T.path.p, T.depth.p, T.slot.p, T.left.p, T.evals.p};
 }
 
 // chain `chain`'s leaf batch of search iteration `it`: buffers by parity, counter per iteration
 BatchView batch_view(spai_engine *e, int chain, uint32_t it) {
     Batch &B = e->batch[chain];
     const size_t h = (size_t)(it & 1u) * B.cap;
-    return BatchView{B.iter_counts.p + it, B.tree.p + h, B.mine.p + h, B.theirs.p + h,
+    return BatchView{B.iter_counts.p + it, B.iter_more.p ? B.iter_more.p + it : nullptr, B.tree.p + h, B.mine.p + h, B.theirs.p + h,
                      B.priors.p + h * kPriorStride, B.value.p + h};
 }
 
@@ -428,14 +480,20 @@ BatchView batch_view(spai_engine *e, int chain, uint32_t it) {
 // kMinChainLeaves leaves per iteration.  (SPAI_CHAINS=k forces up to k chains,
 // for A/B measurements.)  The split never changes results: trees are independent.
 constexpr double kMinChainLeaves = 64;
-// tail mode (select_tree RUN_ON) below this many leaves per iteration in the
-// previous search call; host checks for the end every kTailChunk passes.  A pass
-// lasts as long as its longest terminal run (~3 us per descent), so the mode only
-// pays when hardly any tree still needs evaluations: at 34 and 6.6 leaves per
-// iteration (moves 36 and 37 of a bench step) it took 114 and 49 ms against
-// ~25 and ~18 ms for one launch pair per iteration (profiles/r04/tail)
+// Tail mode (select_tree RUN_ON): a search call runs as passes, one per live leaf
+// of its busiest tree (and at least iterations / kTailRun), each lasting as long
+// as its longest terminal run, at most kTailRun descents (~2.5 us each); the host
+// checks for the end every kTailChunk passes.  So it pays when every tree needs
+// few evaluations: it is chosen when in the previous search call no tree
+// evaluated kTailTreeEvals leaves or more, or the call averaged fewer than
+// kTailLeaves leaves per iteration.  (By the average alone, at 34 and
+// 6.6 leaves per iteration -- moves 36 and 37 of a bench step, where some trees
+// still evaluate most iterations -- it took 114 and 49 ms against ~25 and ~18 ms
+// for one launch pair per iteration: profiles/r04/tail.)
 constexpr double kTailLeaves = 0.05;
 constexpr uint32_t kTailChunk = 4;
+constexpr uint32_t kTailTreeEvals = 160;
+constexpr uint32_t kTailRun = 128;   // terminal descents per tree and pass
 static int env_int(const char *name, int dflt) {
     const char *v = std::getenv(name);
     return v ? std::atoi(v) : dflt;
@@ -550,6 +608,7 @@ int trees_create(spai_engine *e, uint32_t n) {
         SPAI_TRY(T.depth.alloc(n));
         SPAI_TRY(T.slot.alloc(n));
         SPAI_TRY(T.left.alloc(n));
+        SPAI_TRY(T.evals.alloc(n + 1));   // [n]: the search call's max over trees (k_root_stats)
         SPAI_TRY(e->active.alloc(n));
         SPAI_TRY(e->stats.alloc((size_t)n * 8));
         for (Batch &B : e->batch) {   // one double-buffered leaf batch per search chain
@@ -564,6 +623,7 @@ int trees_create(spai_engine *e, uint32_t n) {
         T.cap = (uint32_t)cap;
     }
     e->last_evals_per_iter = -1;   // a fresh set of trees: no per-iteration statistics yet
+    e->last_max_tree_evals = ~0u;
     T.h_root.assign(n, 0);
     T.h_root_state.assign(n, c4::State{0, 0, 0, c4::kOngoing});
     T.h_root_first.assign(n, 0);
@@ -601,21 +661,27 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
     SPAI_CHECK(kind != SPAI_EVAL_NET || e->net, SPAI_ERR_INVALID, "eval = NET but no net set (spai_engine_set_net)");
     if (n == 0) return SPAI_OK;
     hipStream_t st = e->stream;
+    // tail mode (select_tree RUN_ON, one chain): late in a game, when in the previous
+    // search call of these trees no tree evaluated SPAI_TAIL_TREE_EVALS leaves or
+    // more (a pass per live leaf of the busiest tree: few passes), or the call
+    // averaged fewer than SPAI_TAIL_LEAVES leaves per iteration.  Both read per
+    // call (tests set them per case); 0 turns a criterion off.
+    const char *tl_env = std::getenv("SPAI_TAIL_LEAVES");
+    const char *tt_env = std::getenv("SPAI_TAIL_TREE_EVALS");
+    const double tail_leaves = tl_env ? std::atof(tl_env) : kTailLeaves;
+    const uint32_t tail_tree = tt_env ? (uint32_t)std::max(0, std::atoi(tt_env)) : kTailTreeEvals;
+    const char *tr_env = std::getenv("SPAI_TAIL_RUN");
+    const uint32_t tail_run = tr_env ? (uint32_t)std::max(1, std::atoi(tr_env)) : kTailRun;
+    const bool tail = num_searches > 0 && e->last_evals_per_iter >= 0 &&
+                      (e->last_evals_per_iter < tail_leaves || e->last_max_tree_evals < tail_tree);
     // chain h searches active[off[h] .. off[h] + cnt[h]) on chain_stream[h]
-    const ChainPolicy pol = chains_for(n, e->last_evals_per_iter);
+    const ChainPolicy pol = tail ? ChainPolicy{1, 0u} : chains_for(n, e->last_evals_per_iter);
     const int nchain = pol.chains;
     uint32_t off[spai_engine::kChains] = {0, 0, 0, 0}, cnt[spai_engine::kChains] = {0, 0, 0, 0};
     for (int h = 0; h < nchain; ++h) {
         off[h] = (uint32_t)((uint64_t)n * h / nchain);
         cnt[h] = (uint32_t)((uint64_t)n * (h + 1) / nchain) - off[h];
     }
-    // tail mode (select_tree RUN_ON): late in a game, when the previous search call
-    // of these trees evaluated fewer than SPAI_TAIL_LEAVES leaves per iteration
-    // (a single chain then); 0 turns it off
-    const char *tl_env = std::getenv("SPAI_TAIL_LEAVES");   // read per call: tests set it per case
-    const double tail_leaves = tl_env ? std::atof(tl_env) : kTailLeaves;
-    const bool tail = nchain == 1 && num_searches > 0 && e->last_evals_per_iter >= 0 &&
-                      e->last_evals_per_iter < tail_leaves;
     for (int h = 0; h < nchain; ++h) {   // per-iteration leaf counters (also the batch slot counters)
         Batch &B = e->batch[h];
         // at least one counter even for num_searches == 0, so the memset never sees a
@@ -624,9 +690,14 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
         const uint32_t nc = std::max<uint32_t>(num_searches, 1) + (tail ? kTailChunk + 1 : 0);
         if (B.iter_counts.n < nc) SPAI_TRY(B.iter_counts.alloc(nc));
         SPAI_HIP(hipMemsetAsync(B.iter_counts.p, 0, (size_t)nc * 4, st));
+        if (tail) {
+            if (B.iter_more.n < nc) SPAI_TRY(B.iter_more.alloc(nc));
+            SPAI_HIP(hipMemsetAsync(B.iter_more.p, 0, (size_t)nc * 4, st));
+        }
     }
     SPAI_HIP(hipMemcpyAsync(e->active.p, tree_idx, n * 4, hipMemcpyHostToDevice, st));
     SPAI_HIP(hipMemsetAsync(e->err.p, 0, 4, st));
+    SPAI_HIP(hipMemsetAsync(T.evals.p, 0, ((size_t)T.n_trees + 1) * 4, st));
     if (nchain > 1) {   // fork: chains 1.. start after the setup on the engine stream
         SPAI_HIP(hipEventRecord(e->ev_fork, st));
         for (int h = 1; h < nchain; ++h) SPAI_HIP(hipStreamWaitEvent(e->chain_stream[h], e->ev_fork, 0));
@@ -637,14 +708,15 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
     if (tail) {
         // passes on the engine stream: select(0), then per pass p: evaluate(p),
         // expand(p) + select(p + 1), each select running its trees on through
-        // terminal leaves.  A pass whose select slots no leaf leaves no tree with
-        // iterations to run (a tree stops a launch only at a live leaf), so the
-        // host checks every kTailChunk passes and stops there.
+        // terminal leaves (at most tail_run per pass).  A pass whose select slots
+        // no leaf and caps no tree leaves no tree with iterations to run (a tree
+        // stops a launch only at a live leaf or the cap), so the host checks every
+        // kTailChunk passes and stops there.
         const uint32_t g8 = (n + kTreesPerBlock - 1) / kTreesPerBlock;
         const uint32_t *act = e->active.p;
         k_set_left<<<(n + 255) / 256, 256, 0, st>>>(tv, act, n, num_searches);
-        k_select<true><<<g8, kBlock, 0, st>>>(tv, batch_view(e, 0, 0), act, n, e->cfg.c, e->err.p);
-        uint32_t p = 0, next = 1;
+        k_select<true><<<g8, kBlock, 0, st>>>(tv, batch_view(e, 0, 0), act, n, e->cfg.c, e->err.p, tail_run);
+        uint32_t p = 0, next = 1, more = 0;
         for (;;) {
             for (uint32_t q = 0; q < kTailChunk; ++q, ++p) {
                 const BatchView bv = batch_view(e, 0, p);
@@ -654,12 +726,13 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
                     k_eval_stub<<<(n + kBlock - 1) / kBlock, kBlock, 0, st>>>(bv, n, kind);
                 }
                 k_expand_select<true><<<g8, kBlock, 0, st>>>(tv, bv, batch_view(e, 0, p + 1), act, n, e->cfg.c,
-                                                             e->err.p);
+                                                             e->err.p, tail_run);
             }
             SPAI_HIP(hipGetLastError());
             SPAI_HIP(hipMemcpyAsync(&next, e->batch[0].iter_counts.p + p, 4, hipMemcpyDeviceToHost, st));
+            SPAI_HIP(hipMemcpyAsync(&more, e->batch[0].iter_more.p + p, 4, hipMemcpyDeviceToHost, st));
             SPAI_HIP(hipStreamSynchronize(st));
-            if (next == 0) break;   // pass p has nothing to evaluate: every tree is done
+            if (next == 0 && more == 0) break;   // pass p has nothing to evaluate and no tree was capped: all done
             SPAI_CHECK(p <= num_searches + 1, SPAI_ERR_INVALID, "internal: tail passes exceed the iterations");
             // this chunk's counters are read back below; the next chunk's are fresh
         }
@@ -678,7 +751,7 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
             const bool sample = timed && (it % e->timer.stride == 0);
             if (it == 0) {
                 if (sample) SPAI_TRY(timer_record(e, 0, it, true, sh, h));
-                k_select<false><<<g8, kBlock, 0, sh>>>(tv, bv, act, nh, e->cfg.c, e->err.p);
+                k_select<false><<<g8, kBlock, 0, sh>>>(tv, bv, act, nh, e->cfg.c, e->err.p, 0u);
                 if (sample) SPAI_TRY(timer_record(e, 0, it, false, sh, h));
             }
             if (sample) SPAI_TRY(timer_record(e, 1, it, true, sh, h));
@@ -693,7 +766,7 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
                 const bool s2 = timed && ((it + 1) % e->timer.stride == 0);
                 if (s2) SPAI_TRY(timer_record(e, 0, it + 1, true, sh, h));
                 k_expand_select<false><<<g8, kBlock, 0, sh>>>(tv, bv, batch_view(e, h, it + 1), act, nh,
-                                                              e->cfg.c, e->err.p);
+                                                              e->cfg.c, e->err.p, 0u);
                 if (s2) SPAI_TRY(timer_record(e, 0, it + 1, false, sh, h));
             } else {
                 if (sample) SPAI_TRY(timer_record(e, 2, it, true, sh, h));
@@ -707,11 +780,12 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
         SPAI_HIP(hipEventRecord(e->ev_join[h], e->chain_stream[h]));
         SPAI_HIP(hipStreamWaitEvent(st, e->ev_join[h], 0));
     }
-    k_root_stats<<<(n + 255) / 256, 256, 0, st>>>(tv, e->active.p, n, e->stats.p);
+    k_root_stats<<<(n + 255) / 256, 256, 0, st>>>(tv, e->active.p, n, e->stats.p, T.evals.p + T.n_trees);
     SPAI_HIP(hipGetLastError());
     std::vector<uint32_t> stats((size_t)n * 8), counts(n_counts), ch_counts((size_t)nchain * n_counts);
-    uint32_t err = 0;
+    uint32_t err = 0, max_tree_evals = 0;
     SPAI_HIP(hipMemcpyAsync(stats.data(), e->stats.p, stats.size() * 4, hipMemcpyDeviceToHost, st));
+    SPAI_HIP(hipMemcpyAsync(&max_tree_evals, T.evals.p + T.n_trees, 4, hipMemcpyDeviceToHost, st));
     if (n_counts)
         for (int h = 0; h < nchain; ++h)
             SPAI_HIP(hipMemcpyAsync(ch_counts.data() + (size_t)h * n_counts, e->batch[h].iter_counts.p,
@@ -729,6 +803,7 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
         for (uint32_t c : counts) s += c;
         if (evals_out) *evals_out = s;
         e->last_evals_per_iter = num_searches ? s / num_searches : -1;
+        e->last_max_tree_evals = max_tree_evals;
     }
     // root visit policy (mcts.rs:310-331)
     for (uint32_t i = 0; i < n; ++i) {

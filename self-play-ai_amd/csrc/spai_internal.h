@@ -83,6 +83,7 @@ struct Trees {
     DevBuf<uint8_t> depth;          // [n_trees]
     DevBuf<uint32_t> slot;          // [n_trees] leaf slot in the current batch (select -> expand)
     DevBuf<uint32_t> left;          // [n_trees] search iterations left (tail run-on mode, search.hip)
+    DevBuf<uint32_t> evals;         // [n_trees] live leaves of the current search call (tail-mode policy)
     // host mirrors of the root bookkeeping
     std::vector<uint32_t> h_root;
     std::vector<c4::State> h_root_state;
@@ -99,6 +100,7 @@ struct Batch {
     DevBuf<float> priors;           // [cap][8] masked softmax
     DevBuf<float> value;            // [cap]
     DevBuf<uint32_t> iter_counts;   // per-iteration leaf counts of the current search
+    DevBuf<uint32_t> iter_more;     // tail mode: per pass, set if a tree stopped at the run cap
 };
 
 struct KernelTimer {
@@ -198,6 +200,7 @@ struct spai_engine {
     hipEvent_t ev_fork = nullptr, ev_join[kChains] = {nullptr, nullptr, nullptr, nullptr};
     double last_evals_per_iter = -1;   // previous search call's mean leaves per iteration (< 0: none yet)
     uint32_t last_tail_passes = 0;     // previous search call's tail-mode passes (0: not in tail mode)
+    uint32_t last_max_tree_evals = ~0u;   // previous search call's most live leaves of one tree (~0: none yet)
     spai_net *net = nullptr;
     spai::DevBuf<uint32_t> active;   // active tree list
     spai::DevBuf<uint32_t> err;      // device error flags

@@ -407,13 +407,18 @@ def test_self_play_hash_matches_oracle(spai, oracle):
 kTailChunk = 4   # search.hip: passes per host check
 
 
-@pytest.mark.parametrize("tail_leaves", ["8", "64"])
-def test_self_play_tail_mode_matches_oracle(spai, oracle, tmp_path, tail_leaves):
+@pytest.mark.parametrize("tail_leaves,tail_tree,tail_run", [("8", "0", "64"), ("64", "0", "1000"), ("0", "1000", "64"),
+                                                             ("0", "1000", "3")])
+def test_self_play_tail_mode_matches_oracle(spai, oracle, tmp_path, tail_leaves, tail_tree, tail_run):
     """the tail mode (search.hip select_tree RUN_ON): once a search call averages
     fewer than SPAI_TAIL_LEAVES leaves per iteration (default 0.05), the next one
     lets every tree run its iterations on through terminal leaves inside one
-    launch.  Self-play with the hash evaluator on 48 games (one search chain)
-    must still equal the oracle's sample stream bit for bit -- at 8 leaves per
+    launch; or once no tree of the previous call evaluated SPAI_TAIL_TREE_EVALS
+    leaves (default 160; "1000" here: every call after the first).  A tree runs
+    at most SPAI_TAIL_RUN terminal descents per pass (default 128; 3 here: most
+    passes end at the cap, and a pass that slots no leaf does not end the call).
+    Self-play with the hash evaluator on 48 games (one search chain) must still
+    equal the oracle's sample stream bit for bit -- at 8 leaves per
     iteration (the last moves, once fewer than 8 games are left) and at 64, where
     tail-mode moves still hold trees that need evaluations -- and the per-move
     trace must show tail-mode moves (a sixth column of search passes).  (At the
@@ -421,7 +426,8 @@ def test_self_play_tail_mode_matches_oracle(spai, oracle, tmp_path, tail_leaves)
     the other self-play parity tests run the default.)"""
     n, sims, seed = 48, 96, 23
     trace = tmp_path / "moves.csv"
-    env = {"SPAI_TRACE_MOVES": str(trace), "SPAI_TAIL_LEAVES": tail_leaves}
+    env = {"SPAI_TRACE_MOVES": str(trace), "SPAI_TAIL_LEAVES": tail_leaves, "SPAI_TAIL_TREE_EVALS": tail_tree,
+           "SPAI_TAIL_RUN": tail_run}
     os.environ.update(env)
     try:
         e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_HASH, seed=seed)
@@ -444,7 +450,9 @@ def test_self_play_tail_mode_matches_oracle(spai, oracle, tmp_path, tail_leaves)
     rows = [[float(v) for v in l.split(",")] for l in trace.read_text().splitlines()]
     tail = [r for r in rows if r[5] > 0]
     assert tail, "no move ran in tail mode"
-    if tail_leaves == "64":
+    if tail_run == "3":   # every call needs at least sims / 3 passes
+        assert min(r[5] for r in tail) >= sims // 3, [r[5] for r in tail]
+    elif tail_leaves == "64" or tail_tree == "1000":
         assert min(r[5] for r in tail) < sims / 4, [r[5] for r in tail]   # passes, not one per iteration
         # a tail move whose trees still needed evaluations (more than one chunk of passes)
         assert max(r[5] for r in tail) > kTailChunk, [r[5] for r in tail]
