@@ -899,6 +899,39 @@ __host__ __device__ inline int group_size(uint32_t count, uint32_t grid) {
     return g < 1 ? 1 : g > kS ? kS : g;
 }
 
+// Group size when `conc` search chains' forwards share the CUs (conc > 1): their
+// workgroups queue for the same CUs, so the iteration is bound by the forwards'
+// summed CU time as much as by one chain's forward latency plus its tree
+// kernels.  From the latency-optimal size upwards, the size minimising
+// max(conc x CU cycles / grid, forward latency + kChainCycles) on the measured
+// per-group cycles (profiles/r04/search_ab/phases_pro.txt) is taken: larger
+// groups cost fewer CU cycles per leaf (29k at S = 1, 15.7k at S = 4, 12.6k at
+// S = 8).  The results do not depend on S.
+constexpr float kGroupCycles[kS + 1] = {0.f, 29200.f, 45500.f, 58600.f, 62900.f, 81200.f, 86200.f, 94700.f, 100500.f};
+constexpr float kLaunchCycles = 4200.f;   // kernel entry to the first group (~2 us)
+constexpr float kChainCycles = 31000.f;   // the chain's tree kernels and launch gaps per iteration (~15 us)
+// below this many leaves the chains' forwards are short and the model's CU term
+// overstates their contention: measured slower there (moves 26-41 of a bench step,
+// profiles/r04/group_policy)
+constexpr uint32_t kConcMinCount = 600;
+__host__ __device__ inline int group_size_conc(uint32_t count, uint32_t grid, int conc) {
+    const int s0 = group_size(count, grid);
+    if (conc <= 1 || count < kConcMinCount) return s0;
+    float best = 3.0e38f;
+    int bs = s0;
+    for (int S = s0; S <= kS; ++S) {
+        const uint32_t wgs = (count + S - 1) / S, rounds = (wgs + grid - 1) / grid;
+        const float cu = (float)wgs * kGroupCycles[S] + (float)(wgs < grid ? wgs : grid) * kLaunchCycles;
+        const float lat = (float)rounds * kGroupCycles[S] + kLaunchCycles;
+        const float t = fmaxf((float)conc * cu / (float)grid, lat + kChainCycles);
+        if (t < best) {
+            best = t;
+            bs = S;
+        }
+    }
+    return bs;
+}
+
 // The group loop of one (wave, group size) variant.
 template <int W, int S, bool FROM_X>
 __device__ __forceinline__ void run_groups(uint8_t *smem, const NetParams &P, uint32_t count, int ngroups,
@@ -1021,10 +1054,11 @@ __device__ __forceinline__ void dispatch_wave(uint8_t *smem, const NetParams &P,
 
 // Persistent forward: the grid is at most one workgroup per CU; each workgroup
 // loops over groups of S positions (S from the device-side leaf count, see
-// group_size; FROM_X and the diagnostic mode use S = force_s).
+// group_size / group_size_conc for conc concurrent search chains; FROM_X and the
+// diagnostic mode use S = force_s).
 template <bool FROM_X>
 __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict__ count_ptr, uint32_t count_imm,
-                                                      int force_s, const uint64_t *__restrict__ mine,
+                                                      int force_s, int conc, const uint64_t *__restrict__ mine,
                                                       const uint64_t *__restrict__ theirs, const float *__restrict__ x,
                                                       NetParams P, float *__restrict__ priors,
                                                       float *__restrict__ value, float *__restrict__ logits) {
@@ -1041,7 +1075,7 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
 #pragma unroll
     for (int j = 0; j < kBiasPer; ++j) bv[j] = tid + j * kThreads < nbias ? P.b_conv[tid + j * kThreads] : 0.f;
     const uint32_t count = count_ptr ? *count_ptr : count_imm;
-    const int S = force_s > 0 ? force_s : group_size(count, gridDim.x);
+    const int S = force_s > 0 ? force_s : group_size_conc(count, gridDim.x, conc);
     const int ngroups = (int)((count + S - 1) / S);
     if ((int)blockIdx.x >= ngroups) return;
     if (tid < 64) ((uint32_t *)(smem + kZ))[tid] = 0u;   // the zero blocks below X and Y
@@ -1404,7 +1438,7 @@ int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
     NetParams P = params_of(n);
     P.stamps = d.p;
     for (int rep = 0; rep < 3; ++rep)   // last launch warm
-        k_forward<false><<<grid, kThreads, 0, st>>>(nullptr, cnt, S, n->io_mine.p, n->io_theirs.p, nullptr, P,
+        k_forward<false><<<grid, kThreads, 0, st>>>(nullptr, cnt, S, 1, n->io_mine.p, n->io_theirs.p, nullptr, P,
                                                    n->io_priors.p, n->io_value.p, nullptr);
     SPAI_HIP(hipGetLastError());
     std::vector<unsigned long long> hs(d.n);
@@ -1435,7 +1469,7 @@ int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
 }
 
 int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint32_t max_n, const uint64_t *mine,
-                   const uint64_t *theirs, float *priors, float *value, uint32_t grid_cap_call) {
+                   const uint64_t *theirs, float *priors, float *value, uint32_t grid_cap_call, int conc) {
     if (!max_n) return SPAI_OK;
     if (net->dtype == SPAI_DTYPE_F32) return net_f32_launch(net, st, d_count, max_n, mine, theirs, nullptr, priors, value, nullptr);
     // SPAI_FWD_GRID caps the persistent grid (tuning knob: fewer workgroups -> larger groups S)
@@ -1446,8 +1480,13 @@ int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint3
     uint32_t grid = std::min<uint32_t>(max_n, (uint32_t)net->n_cu);
     if (grid_cap) grid = std::min(grid, grid_cap);
     if (grid_cap_call) grid = std::min(grid, grid_cap_call);
-    k_forward<false><<<grid, kThreads, 0, st>>>(d_count, max_n, 0, mine, theirs, nullptr, params_of(net), priors,
-                                                value, nullptr);
+    // SPAI_FWD_CONC=0: the latency-optimal group size whatever the chains (A/B knob)
+    static const bool conc_policy = [] {
+        const char *v = std::getenv("SPAI_FWD_CONC");
+        return !v || std::atoi(v) != 0;
+    }();
+    k_forward<false><<<grid, kThreads, 0, st>>>(d_count, max_n, 0, conc_policy ? conc : 1, mine, theirs, nullptr,
+                                                params_of(net), priors, value, nullptr);
     SPAI_HIP(hipGetLastError());
     return SPAI_OK;
 }
@@ -1461,7 +1500,7 @@ int net_forward_x(spai_net *n, uint32_t cnt, const float *x, float *logits, floa
     if (n->dtype == SPAI_DTYPE_F32) {
         SPAI_TRY(net_f32_launch(n, st, nullptr, cnt, nullptr, nullptr, n->io_x.p, nullptr, n->io_value.p, n->io_logits.p));
     } else {
-        k_forward<true><<<(cnt + kS - 1) / kS, kThreads, 0, st>>>(nullptr, cnt, kS, nullptr, nullptr, n->io_x.p,
+        k_forward<true><<<(cnt + kS - 1) / kS, kThreads, 0, st>>>(nullptr, cnt, kS, 1, nullptr, nullptr, n->io_x.p,
                                                                  params_of(n), nullptr, n->io_value.p, n->io_logits.p);
         SPAI_HIP(hipGetLastError());
     }
@@ -1488,7 +1527,7 @@ int net_predict(spai_net *n, uint32_t cnt, const spai_c4_state *states, float *p
                                 n->io_value.p, nullptr));
     } else {
         k_forward<false><<<std::min<uint32_t>(cnt, (uint32_t)n->n_cu), kThreads, 0, st>>>(
-            nullptr, cnt, 0, n->io_mine.p, n->io_theirs.p, nullptr, params_of(n), n->io_priors.p, n->io_value.p,
+            nullptr, cnt, 0, 1, n->io_mine.p, n->io_theirs.p, nullptr, params_of(n), n->io_priors.p, n->io_value.p,
             nullptr);
         SPAI_HIP(hipGetLastError());
     }

@@ -757,7 +757,7 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
             if (sample) SPAI_TRY(timer_record(e, 1, it, true, sh, h));
             if (kind == SPAI_EVAL_NET) {
                 SPAI_TRY(net_eval_batch(e->net, sh, bv.count, nh, bv.mine, bv.theirs, bv.priors, bv.value,
-                                        pol.grid_cap));
+                                        pol.grid_cap, nchain));
             } else {
                 k_eval_stub<<<(nh + kBlock - 1) / kBlock, kBlock, 0, sh>>>(bv, nh, kind);
             }

@@ -231,9 +231,11 @@ size_t net_num_params(int game, int blocks, int hidden);
 int net_phase_stamps(spai_net *net, uint32_t n, double *cycles);
 int net_bench(spai_net *net, uint32_t n, uint32_t iters, double *ms);
 void net_init_params(int game, int blocks, int hidden, uint64_t seed, float *params);
-// evaluate `count` (device scalar) leaves of the batch; grid sized for max_n
+// evaluate `count` (device scalar) leaves of the batch; grid sized for max_n; conc:
+// search chains whose forwards share the CUs (the group-size policy, net_c4.hip)
 int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint32_t max_n,
-                   const uint64_t *mine, const uint64_t *theirs, float *priors, float *value, uint32_t grid_cap = 0);
+                   const uint64_t *mine, const uint64_t *theirs, float *priors, float *value, uint32_t grid_cap = 0,
+                   int conc = 1);
 
 // net_c4_f32.hip
 int net_create_f32(spai_net *n, const float *params);
