@@ -909,11 +909,17 @@ __host__ __device__ inline int group_size(uint32_t count, uint32_t grid) {
 // S = 8).  The results do not depend on S.
 constexpr float kGroupCycles[kS + 1] = {0.f, 29200.f, 45500.f, 58600.f, 62900.f, 81200.f, 86200.f, 94700.f, 100500.f};
 constexpr float kLaunchCycles = 4200.f;   // kernel entry to the first group (~2 us)
-constexpr float kChainCycles = 31000.f;   // the chain's tree kernels and launch gaps per iteration (~15 us)
+#ifndef SPAI_CONC_CHAIN_CYCLES
+#define SPAI_CONC_CHAIN_CYCLES 31000.f
+#endif
+#ifndef SPAI_CONC_MIN_COUNT
+#define SPAI_CONC_MIN_COUNT 600
+#endif
+constexpr float kChainCycles = SPAI_CONC_CHAIN_CYCLES;   // the chain's tree kernels and launch gaps per iteration (~15 us)
 // below this many leaves the chains' forwards are short and the model's CU term
 // overstates their contention: measured slower there (moves 26-41 of a bench step,
 // profiles/r04/group_policy)
-constexpr uint32_t kConcMinCount = 600;
+constexpr uint32_t kConcMinCount = SPAI_CONC_MIN_COUNT;
 __host__ __device__ inline int group_size_conc(uint32_t count, uint32_t grid, int conc) {
     const int s0 = group_size(count, grid);
     if (conc <= 1 || count < kConcMinCount) return s0;
