@@ -175,6 +175,8 @@ int spai_engine_destroy(spai_engine *e) {
     T.path.release();
     T.depth.release();
     T.slot.release();
+    T.left.release();
+    T.evals.release();
     for (Batch &B : e->batch) {
         B.tree.release();
         B.mine.release();
