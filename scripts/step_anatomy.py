@@ -1,5 +1,6 @@
 """Anatomy of one self-play step from a rocprofv3 --kernel-trace CSV: the step is
-cut into moves at each k_root_stats (one per search call), and per move the
+cut into moves at each k_advance (self-play's move step; k_root_stats in builds
+before it: one per search call), and per move the
 script reports the wall time, the forward (k_forward) launches with their mean
 duration, the tree-kernel launches (k_select / k_expand_select / k_expand) with
 theirs, and how the wall splits into time with 0, 1 or 2 forwards running.
@@ -26,7 +27,7 @@ def main():
     moves, cur = [], []
     for k in ks:
         cur.append(k)
-        if k[2] == "k_root_stats":
+        if k[2] in ("k_advance", "k_root_stats"):
             moves.append(cur)
             cur = []
     out = []

@@ -193,6 +193,10 @@ int spai_engine_destroy(spai_engine *e) {
     e->active.release();
     e->err.release();
     e->stats.release();
+    e->pow_tab.release();
+    e->move_out.release();
+    for (uint32_t *&h : e->h_move)
+        if (h) (void)hipHostFree(h);
     for (hipEvent_t ev : e->timer.ev) (void)hipEventDestroy(ev);
     for (int h = 1; h < spai_engine::kChains; ++h) {
         if (e->chain_stream[h]) (void)hipStreamSynchronize(e->chain_stream[h]);

@@ -1,4 +1,4 @@
-// philox.h — move sampling for self-play (host side).
+// philox.h — move sampling for self-play (host, and the device for Connect4).
 //
 // The reference samples a root child with rand::thread_rng and
 // WeightedIndex over visit_count^temperature (learner_concurrent.rs:177,189-193),
@@ -13,9 +13,16 @@
 #include <cmath>
 #include <vector>
 
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define SPAI_PHX __host__ __device__ inline
+#else
+#define SPAI_PHX inline
+#endif
+
 namespace spai {
 
-inline void philox4x32(uint32_t c[4], const uint32_t key[2], uint32_t out[4]) {
+SPAI_PHX void philox4x32(uint32_t c[4], const uint32_t key[2], uint32_t out[4]) {
     uint32_t c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3], k0 = key[0], k1 = key[1];
     for (int r = 0; r < 10; ++r) {
         uint64_t p0 = (uint64_t)0xD2511F53u * c0;
@@ -29,7 +36,7 @@ inline void philox4x32(uint32_t c[4], const uint32_t key[2], uint32_t out[4]) {
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-inline double sample_uniform(uint64_t seed, uint64_t game_id, uint64_t move_no) {
+SPAI_PHX double sample_uniform(uint64_t seed, uint64_t game_id, uint64_t move_no) {
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
     uint32_t ctr[4] = {(uint32_t)move_no, (uint32_t)(move_no >> 32), (uint32_t)game_id, (uint32_t)(game_id >> 32)};
     uint32_t out[4];
@@ -57,6 +64,18 @@ struct PowCache {
     }
 };
 
+// the sampled index from the running sums cum[0..n) of the weights (total = cum[n-1])
+SPAI_PHX int weighted_index_cum(const double *cum, int n, double total, double u) {
+    if (!(total > 0.0)) return -2;
+    double x = u * total;
+    int last = 0;   // last index whose cumulative weight increased (rand never picks a zero weight)
+    for (int i = 0; i < n; ++i) {
+        if (cum[i] > x) return i;
+        if (i == 0 ? cum[0] > 0.0 : cum[i] > cum[i - 1]) last = i;
+    }
+    return last;   // u * total rounded up to total
+}
+
 template <class Pow>
 inline int weighted_index_with(const float *visits, int n, float temperature, double u, Pow &&pw) {
     double cum[512];
@@ -66,14 +85,7 @@ inline int weighted_index_with(const float *visits, int n, float temperature, do
         total += pw(visits[i], temperature);
         cum[i] = total;
     }
-    if (!(total > 0.0)) return -2;
-    double x = u * total;
-    int last = 0;   // last index whose cumulative weight increased (rand never picks a zero weight)
-    for (int i = 0; i < n; ++i) {
-        if (cum[i] > x) return i;
-        if (i == 0 ? cum[0] > 0.0 : cum[i] > cum[i - 1]) last = i;
-    }
-    return last;   // u * total rounded up to total
+    return weighted_index_cum(cum, n, total, u);
 }
 
 inline int weighted_index(const float *visits, int n, float temperature, double u) {

@@ -21,7 +21,8 @@
 // Leaf batches are double-buffered by iteration parity, and every iteration
 // has its own slot counter (zeroed once per search call).
 // The host only sees the trees between moves: root visit counts come back once
-// per search call, the sampled child goes down as the new root.
+// per search call.  In self-play the move is sampled on the device too
+// (k_advance), which writes the sampled child as the new root.
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -451,6 +452,82 @@ __global__ void k_root_stats(TreeView T, const uint32_t *__restrict__ active, ui
     for (uint32_t k = 0; k < 7; ++k) out[i * 8 + 1 + k] = k < nch ? nodes[first + k].x : 0u;
 }
 
+// Self-play's move after a search call (learner_concurrent.rs:177-203), per active
+// tree: the root's visit counts, the sampled child (the Philox uniform of philox.h
+// and WeightedIndex over visits^T, the weights from the host's std::pow table, so
+// the pick is the host sampler's bit for bit), and for a game that goes on the
+// child written as the tree's new root (use_subtree).  One record per tree goes
+// back to the host: [0] the root's children word, [1..7] the child visit counts,
+// [8] the pick (index | action << 8 | new status << 16; without one, bit 31 and
+// the weighted_index code, or kPickNoTable for a visit count beyond the table),
+// [9] the tree's live leaves of the call.  out[0] gets the error flags, and
+// block 0 copies every chain's per-iteration leaf counts after the records, so
+// one copy brings back everything the host needs.
+constexpr int kMoveRec = 10;
+constexpr uint32_t kPickNone = 0x80000000u, kPickNoTable = 3u;
+struct RootsOut {
+    uint32_t *root;
+    uint64_t *x, *o;
+    uint8_t *n, *status;
+};
+struct ChainCounts {
+    const uint32_t *p[spai_engine::kChains];
+};
+__global__ void k_advance(TreeView T, RootsOut R, const uint32_t *__restrict__ active, uint32_t n_active,
+                          const double *__restrict__ pow_tab, uint32_t pow_n, uint64_t seed, uint64_t gid_base,
+                          uint64_t move_no, const uint32_t *err, ChainCounts cc, int nchain, uint32_t n_counts,
+                          uint32_t *out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) {
+            out[0] = *err;
+            out[1] = 0;
+        }
+        uint32_t *counts = out + 2 + (size_t)n_active * kMoveRec;
+        for (int h = 0; h < nchain; ++h)
+            for (uint32_t j = threadIdx.x; j < n_counts; j += blockDim.x) counts[(size_t)h * n_counts + j] = cc.p[h][j];
+    }
+    if (i >= n_active) return;
+    const uint32_t t = active[i];
+    const uint4 *nodes = T.nodes + (size_t)t * T.cap;
+    const uint4 r = nodes[T.root[t]];
+    const uint32_t nch = r.w == kNoChildren ? 0 : r.w >> 24, first = r.w & 0xFFFFFFu;
+    uint32_t vis[c4::kActions];
+#pragma unroll
+    for (int k = 0; k < c4::kActions; ++k) vis[k] = (uint32_t)k < nch ? nodes[first + k].x : 0u;
+    uint32_t *rec = out + 2 + (size_t)i * kMoveRec;
+    rec[0] = r.w;
+#pragma unroll
+    for (int k = 0; k < c4::kActions; ++k) rec[1 + k] = vis[k];
+    rec[9] = T.evals[t];
+    bool beyond = false;
+    int idx = -1;   // weighted_index_with: -1 without children
+    if (nch > 0) {
+        double cum[c4::kActions], total = 0.0;
+        for (uint32_t k = 0; k < nch; ++k) {
+            beyond |= vis[k] >= pow_n;
+            total += pow_tab[min(vis[k], pow_n - 1)];
+            cum[k] = total;
+        }
+        idx = weighted_index_cum(cum, (int)nch, total, sample_uniform(seed, gid_base + t, move_no));
+    }
+    if (beyond || idx < 0) {
+        rec[8] = kPickNone | (beyond ? kPickNoTable : (uint32_t)(-idx));
+        return;
+    }
+    const c4::State rs{T.root_x[t], T.root_o[t], T.root_n[t], T.root_status[t]};
+    const int a = c4::kth_bit(c4::legal_mask(rs.x, rs.o, rs.status), idx);
+    c4::State cs = rs;
+    (void)c4::next_state(rs, a, cs);
+    rec[8] = (uint32_t)idx | (uint32_t)a << 8 | (uint32_t)cs.status << 16;
+    if (cs.status == c4::kOngoing) {
+        R.root[t] = first + (uint32_t)idx;
+        R.x[t] = cs.x;
+        R.o[t] = cs.o;
+        R.n[t] = cs.n;
+        R.status[t] = cs.status;
+    }
+}
 __global__ void k_trees_init(TreeView T, uint32_t first_tree, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -566,7 +643,7 @@ int timer_record(spai_engine *e, int which, uint32_t iter, bool begin, hipStream
 
 // fold the sampled event pairs of one search call into the totals
 // ch_counts [chain][num_searches] leaves per iteration; n_active[chain] trees
-int timer_collect(spai_engine *e, const std::vector<uint32_t> &ch_counts, uint32_t num_searches,
+int timer_collect(spai_engine *e, const uint32_t *ch_counts, uint32_t num_searches,
                   const uint32_t *n_active) {
     KernelTimer &K = e->timer;
     if (!K.enabled) return SPAI_OK;
@@ -651,15 +728,28 @@ int tree_reset(spai_engine *e, uint32_t t, const spai_c4_state *root) {
     return upload_roots(e, t, 1);
 }
 
-int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_searches, float *policy,
-           uint32_t *child_ids, float *child_visits, uint32_t *n_children, double *evals_out) {
+namespace {
+// Policy::normalize: ndarray sum (sequential for 7) then divide
+inline void normalize_policy(const float (&pol)[c4::kActions], float *out) {
+    float s = 0.0f;
+    for (int a = 0; a < c4::kActions; ++a) s = s + pol[a];
+    for (int a = 0; a < c4::kActions; ++a) out[a] = pol[a] / s;
+}
+
+// one search call's launch layout, for search_finish
+struct SearchRun {
+    int nchain = 1;
+    bool tail = false;
+    uint32_t n_counts = 0;                                  // per-iteration leaf counters per chain
+    uint32_t cnt[spai_engine::kChains] = {0, 0, 0, 0};      // trees per chain
+};
+
+// Enqueue one search call over n >= 1 validated trees (mcts.rs:214-285 per tree),
+// up to the join of its chains on the engine stream.  Only tail mode waits (once
+// per chunk of passes, for its stop condition).
+int search_launch(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_searches, SearchRun &R) {
     Trees &T = e->trees;
-    SPAI_CHECK(T.n_trees > 0, SPAI_ERR_INVALID, "no trees: call spai_trees_create first");
-    SPAI_CHECK(n <= T.n_trees, SPAI_ERR_INVALID, "search over %u trees, %u exist", n, T.n_trees);
-    for (uint32_t i = 0; i < n; ++i) SPAI_CHECK(tree_idx[i] < T.n_trees, SPAI_ERR_INVALID, "tree %u out of range", tree_idx[i]);
     const int kind = (int)e->cfg.eval;
-    SPAI_CHECK(kind != SPAI_EVAL_NET || e->net, SPAI_ERR_INVALID, "eval = NET but no net set (spai_engine_set_net)");
-    if (n == 0) return SPAI_OK;
     hipStream_t st = e->stream;
     // tail mode (select_tree RUN_ON, one chain): late in a game, when in the previous
     // search call of these trees no tree evaluated SPAI_TAIL_TREE_EVALS leaves or
@@ -677,7 +767,10 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
     // chain h searches active[off[h] .. off[h] + cnt[h]) on chain_stream[h]
     const ChainPolicy pol = tail ? ChainPolicy{1, 0u} : chains_for(n, e->last_evals_per_iter);
     const int nchain = pol.chains;
-    uint32_t off[spai_engine::kChains] = {0, 0, 0, 0}, cnt[spai_engine::kChains] = {0, 0, 0, 0};
+    uint32_t off[spai_engine::kChains] = {0, 0, 0, 0};
+    uint32_t *cnt = R.cnt;
+    R.nchain = nchain;
+    R.tail = tail;
     for (int h = 0; h < nchain; ++h) {
         off[h] = (uint32_t)((uint64_t)n * h / nchain);
         cnt[h] = (uint32_t)((uint64_t)n * (h + 1) / nchain) - off[h];
@@ -704,7 +797,8 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
     }
     const TreeView tv = tree_view(e);
     const bool timed = e->timer.enabled && !tail;   // samples every chain's launches every stride-th iteration
-    uint32_t n_counts = num_searches;   // leaf counters to read back per chain
+    uint32_t &n_counts = R.n_counts;   // leaf counters to read back per chain
+    n_counts = num_searches;
     if (tail) {
         // passes on the engine stream: select(0), then per pass p: evaluate(p),
         // expand(p) + select(p + 1), each select running its trees on through
@@ -780,9 +874,46 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
         SPAI_HIP(hipEventRecord(e->ev_join[h], e->chain_stream[h]));
         SPAI_HIP(hipStreamWaitEvent(st, e->ev_join[h], 0));
     }
+    return SPAI_OK;
+}
+
+// The call's bookkeeping once its counters [chain][n_counts], error flags and
+// largest per-tree leaf count are on the host: timers, the device errors, and the
+// statistics the next call's chain and tail policies read.
+int search_finish(spai_engine *e, const SearchRun &R, uint32_t num_searches, const uint32_t *ch_counts, uint32_t err,
+                  uint32_t max_tree_evals, double *evals_out) {
+    SPAI_TRY(timer_collect(e, ch_counts, R.n_counts, R.cnt));
+    double s = 0;
+    for (int h = 0; h < R.nchain; ++h)
+        for (uint32_t i = 0; i < R.n_counts; ++i) s += ch_counts[(size_t)h * R.n_counts + i];
+    SPAI_CHECK(!(err & kErrCapacity), SPAI_ERR_CAPACITY, "node arena full (cap %u per tree)", e->trees.cap);
+    SPAI_CHECK(!(err & kErrDepth), SPAI_ERR_CAPACITY, "tree deeper than %d", kMaxDepth);
+    SPAI_CHECK(!(err & kErrNan), SPAI_ERR_NAN, "NaN UCB in select (reference: partial_cmp().unwrap() panics)");
+    if (evals_out) *evals_out = s;
+    e->last_evals_per_iter = num_searches ? s / num_searches : -1;
+    e->last_max_tree_evals = max_tree_evals;
+    return SPAI_OK;
+}
+}  // namespace
+
+int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_searches, float *policy,
+           uint32_t *child_ids, float *child_visits, uint32_t *n_children, double *evals_out) {
+    Trees &T = e->trees;
+    SPAI_CHECK(T.n_trees > 0, SPAI_ERR_INVALID, "no trees: call spai_trees_create first");
+    SPAI_CHECK(n <= T.n_trees, SPAI_ERR_INVALID, "search over %u trees, %u exist", n, T.n_trees);
+    for (uint32_t i = 0; i < n; ++i) SPAI_CHECK(tree_idx[i] < T.n_trees, SPAI_ERR_INVALID, "tree %u out of range", tree_idx[i]);
+    const int kind = (int)e->cfg.eval;
+    SPAI_CHECK(kind != SPAI_EVAL_NET || e->net, SPAI_ERR_INVALID, "eval = NET but no net set (spai_engine_set_net)");
+    if (n == 0) return SPAI_OK;
+    hipStream_t st = e->stream;
+    SearchRun R;
+    SPAI_TRY(search_launch(e, n, tree_idx, num_searches, R));
+    const TreeView tv = tree_view(e);
+    const int nchain = R.nchain;
+    const uint32_t n_counts = R.n_counts;
     k_root_stats<<<(n + 255) / 256, 256, 0, st>>>(tv, e->active.p, n, e->stats.p, T.evals.p + T.n_trees);
     SPAI_HIP(hipGetLastError());
-    std::vector<uint32_t> stats((size_t)n * 8), counts(n_counts), ch_counts((size_t)nchain * n_counts);
+    std::vector<uint32_t> stats((size_t)n * 8), ch_counts((size_t)nchain * n_counts);
     uint32_t err = 0, max_tree_evals = 0;
     SPAI_HIP(hipMemcpyAsync(stats.data(), e->stats.p, stats.size() * 4, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipMemcpyAsync(&max_tree_evals, T.evals.p + T.n_trees, 4, hipMemcpyDeviceToHost, st));
@@ -792,19 +923,7 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
                                     n_counts * 4, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipMemcpyAsync(&err, e->err.p, 4, hipMemcpyDeviceToHost, st));
     SPAI_HIP(hipStreamSynchronize(st));
-    SPAI_TRY(timer_collect(e, ch_counts, n_counts, cnt));
-    for (int h = 0; h < nchain; ++h)
-        for (uint32_t i = 0; i < n_counts; ++i) counts[i] += ch_counts[(size_t)h * n_counts + i];
-    SPAI_CHECK(!(err & kErrCapacity), SPAI_ERR_CAPACITY, "node arena full (cap %u per tree)", T.cap);
-    SPAI_CHECK(!(err & kErrDepth), SPAI_ERR_CAPACITY, "tree deeper than %d", kMaxDepth);
-    SPAI_CHECK(!(err & kErrNan), SPAI_ERR_NAN, "NaN UCB in select (reference: partial_cmp().unwrap() panics)");
-    {
-        double s = 0;
-        for (uint32_t c : counts) s += c;
-        if (evals_out) *evals_out = s;
-        e->last_evals_per_iter = num_searches ? s / num_searches : -1;
-        e->last_max_tree_evals = max_tree_evals;
-    }
+    SPAI_TRY(search_finish(e, R, num_searches, ch_counts.data(), err, max_tree_evals, evals_out));
     // root visit policy (mcts.rs:310-331)
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t t = tree_idx[i];
@@ -826,11 +945,7 @@ int search(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t num_se
             if (child_visits) child_visits[(size_t)i * 7 + k] = 0.f;
         }
         if (n_children) n_children[i] = nch;
-        if (policy) {
-            float s = 0.0f;   // Policy::normalize: ndarray sum (sequential for 7) then divide
-            for (int a = 0; a < c4::kActions; ++a) s = s + pol[a];
-            for (int a = 0; a < c4::kActions; ++a) policy[(size_t)i * 7 + a] = pol[a] / s;
-        }
+        if (policy) normalize_policy(pol, policy + (size_t)i * 7);
     }
     return SPAI_OK;
 }
@@ -881,55 +996,149 @@ int tree_size(spai_engine *e, uint32_t t, uint32_t *nodes) {
     return SPAI_OK;
 }
 
-// SelfPlayWorker::self_play (learner_concurrent.rs:169-242)
+// SelfPlayWorker::self_play (learner_concurrent.rs:169-242).  Per move: the search
+// call, then k_advance samples every game's move on the device and moves its
+// root, and one pinned copy brings back the records.  The next move's search is
+// launched as soon as the host knows which games go on; this move's bookkeeping
+// (policy targets, histories, finished games to the sink, in the reference's
+// order) runs on the host while it searches.
 int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sample_sink sink, void *user,
                  spai_selfplay_stats *stats) {
     const auto t_start = std::chrono::steady_clock::now();
     SPAI_TRY(trees_create(e, n_games));
+    SPAI_CHECK(e->cfg.eval != SPAI_EVAL_NET || e->net, SPAI_ERR_INVALID,
+               "eval = NET but no net set (spai_engine_set_net)");
     Trees &T = e->trees;
+    hipStream_t st = e->stream;
+    const uint32_t ns = e->cfg.num_searches;
     // every game's history in flat per-game slabs of the longest game (42 plies):
     // growing 3 x n_games vectors made every game reallocate at the same moves
     constexpr size_t kPlies = c4::kCells;
+    // visits^T for every count a root child can reach (a search call adds at most
+    // ns visits to a root, a game has at most kPlies moves), by the std::pow the
+    // host sampler used, once per temperature
+    const uint32_t pow_n = ns * (uint32_t)kPlies + 1;
+    const double temp = (double)e->cfg.temperature;
+    if (e->pow_tab_t != temp || e->pow_tab.n < pow_n) {
+        std::vector<double> tab(pow_n);
+        for (uint32_t k = 0; k < pow_n; ++k) tab[k] = std::pow((double)k, temp);
+        e->pow_tab_t = -1.0;
+        SPAI_TRY(e->pow_tab.alloc(pow_n));
+        SPAI_HIP(hipMemcpy(e->pow_tab.p, tab.data(), pow_n * sizeof(double), hipMemcpyHostToDevice));
+        e->pow_tab_t = temp;
+    }
+    // records, then every chain's leaf counters (tail mode: up to ns + kTailChunk + 1)
+    const size_t n_words = 2 + (size_t)n_games * kMoveRec +
+                           (size_t)spai_engine::kChains * (std::max(ns, 1u) + kTailChunk + 1);
+    if (e->h_move_n < n_words) {
+        e->h_move_n = 0;
+        for (uint32_t *&h : e->h_move) {
+            if (h) (void)hipHostFree(h);
+            h = nullptr;
+            void *ph = nullptr;
+            SPAI_HIP(hipHostMalloc(&ph, n_words * 4, hipHostMallocDefault));
+            h = (uint32_t *)ph;
+        }
+        SPAI_TRY(e->move_out.alloc(n_words));
+        e->h_move_n = n_words;
+    }
     std::vector<c4::State> h_states((size_t)n_games * kPlies);
     std::vector<float> h_pol((size_t)n_games * kPlies * 7);
     std::vector<int32_t> h_moves((size_t)n_games * kPlies);
     std::vector<uint32_t> h_len(n_games, 0);
-    std::vector<uint32_t> active(n_games);
-    for (uint32_t i = 0; i < n_games; ++i) active[i] = i;
-    std::vector<float> pol((size_t)n_games * 7), vis((size_t)n_games * 7);
-    std::vector<uint32_t> ids((size_t)n_games * 7), nch(n_games);
-    std::vector<float> enc, sp, sv;
+    std::vector<uint32_t> act[2];   // this move's trees and the next move's (the launch reads them)
+    act[0].resize(n_games);
+    for (uint32_t i = 0; i < n_games; ++i) act[0][i] = i;
+    std::vector<float> enc, sv;
     double sims = 0, evals = 0, games = 0, positions = 0, moves = 0;
-    uint64_t move_no = 0;
-    PowCache pow_cache;   // visits^T of the sampling, once per visit count (was ~0.5 ms of std::pow per move)
     // optional per-move trace (diagnostics): SPAI_TRACE_MOVES=<csv path>
     FILE *trace = nullptr;
     if (const char *tp = std::getenv("SPAI_TRACE_MOVES")) trace = std::fopen(tp, "a");
-    while (!active.empty()) {
-        const uint32_t na = (uint32_t)active.size();
-        double ev = 0;
-        const auto tm0 = std::chrono::steady_clock::now();
-        SPAI_TRY(search(e, na, active.data(), e->cfg.num_searches, pol.data(), ids.data(), vis.data(), nch.data(), &ev));
+    struct TraceClose {
+        FILE *f;
+        ~TraceClose() {
+            if (f) std::fclose(f);
+        }
+    } trace_close{trace};
+    const TreeView tv = tree_view(e);
+    const RootsOut ro{T.root.p, T.root_x.p, T.root_o.p, T.root_n.p, T.root_status.p};
+    SearchRun R;
+    // enqueue move mv over the trees a: the search call, k_advance, the records' copy to dst
+    auto launch = [&](const std::vector<uint32_t> &a, uint64_t mv, uint32_t *dst) -> int {
+        const uint32_t na = (uint32_t)a.size();
+        SPAI_TRY(search_launch(e, na, a.data(), ns, R));
+        ChainCounts cc{};
+        for (int h = 0; h < R.nchain; ++h) cc.p[h] = e->batch[h].iter_counts.p;
+        k_advance<<<(na + 63) / 64, 64, 0, st>>>(tv, ro, e->active.p, na, e->pow_tab.p, (uint32_t)e->pow_tab.n,
+                                                 e->cfg.seed, gid_base, mv, e->err.p, cc, R.nchain, R.n_counts,
+                                                 e->move_out.p);
+        SPAI_HIP(hipGetLastError());
+        const size_t words = 2 + (size_t)na * kMoveRec + (size_t)R.nchain * R.n_counts;
+        SPAI_HIP(hipMemcpyAsync(dst, e->move_out.p, words * 4, hipMemcpyDeviceToHost, st));
+        return SPAI_OK;
+    };
+    uint64_t move_no = 0;
+    int cur = 0;
+    auto tm0 = std::chrono::steady_clock::now();
+    SPAI_TRY(launch(act[0], 0, e->h_move[0]));
+    while (!act[cur].empty()) {
+        const std::vector<uint32_t> &A = act[cur];
+        const uint32_t na = (uint32_t)A.size();
+        const uint32_t *mo = e->h_move[move_no & 1];
+        SPAI_HIP(hipStreamSynchronize(st));
         const auto tm1 = std::chrono::steady_clock::now();
-        sims += (double)na * e->cfg.num_searches;
+        const uint32_t passes = e->last_tail_passes;
+        uint32_t max_ev = 0;
+        bool stop = false;   // a game without a move: its error is raised in the bookkeeping below
+        for (uint32_t i = 0; i < na; ++i) {
+            const uint32_t *rec = mo + 2 + (size_t)i * kMoveRec;
+            max_ev = std::max(max_ev, rec[9]);
+            stop |= (rec[8] & kPickNone) != 0;
+        }
+        double ev = 0;
+        SPAI_TRY(search_finish(e, R, ns, mo + 2 + (size_t)na * kMoveRec, mo[0], max_ev, &ev));
+        sims += (double)na * ns;
         evals += ev;
         moves += 1;
-        for (int k = (int)na - 1; k >= 0; --k) {              // for i in (0..trees_vec.len()).rev()
-            const uint32_t t = active[k];
-            const double u = sample_uniform(e->cfg.seed, gid_base + t, move_no);
-            const int idx = weighted_index_with(vis.data() + (size_t)k * 7, (int)nch[k], e->cfg.temperature, u, pow_cache);
-            SPAI_CHECK(idx >= 0, SPAI_ERR_NAN, "WeightedIndex over all-zero visit counts (game %u)", t);
+        // the games that go on, in order (trees_vec.remove keeps it), and their next move
+        std::vector<uint32_t> &N = act[cur ^ 1];
+        N.clear();
+        auto tm2 = tm1;
+        if (!stop) {
+            for (uint32_t i = 0; i < na; ++i)
+                if (((mo[2 + (size_t)i * kMoveRec + 8] >> 16) & 0xFFu) == c4::kOngoing) N.push_back(A[i]);
+            tm2 = std::chrono::steady_clock::now();
+            if (!N.empty()) SPAI_TRY(launch(N, move_no + 1, e->h_move[(move_no + 1) & 1]));
+        }
+        const auto tm3 = std::chrono::steady_clock::now();
+        for (int k = (int)na - 1; k >= 0; --k) {   // for i in (0..trees_vec.len()).rev()
+            const uint32_t t = A[k];
+            const uint32_t *rec = mo + 2 + (size_t)k * kMoveRec;
+            const uint32_t w = rec[0], pick = rec[8];
+            if (pick & kPickNone) {
+                SPAI_CHECK((pick & 0xFFu) != kPickNoTable, SPAI_ERR_INVALID,
+                           "internal: game %u has a visit count beyond the visits^T table", t);
+                SPAI_CHECK(false, SPAI_ERR_NAN, "WeightedIndex over all-zero visit counts (game %u)", t);
+            }
+            const uint32_t nch = w == kNoChildren ? 0 : w >> 24, first = w & 0xFFFFFFu;
+            T.h_root_first[t] = first;
+            T.h_root_nch[t] = (uint8_t)nch;
             const c4::State rs = T.h_root_state[t];
-            const int a = c4::kth_bit(c4::legal_mask(rs.x, rs.o, rs.status), idx);
+            const uint32_t legal = c4::legal_mask(rs.x, rs.o, rs.status);
+            float pol[c4::kActions] = {0, 0, 0, 0, 0, 0, 0};   // root visit policy (mcts.rs:310-331)
+            for (uint32_t j = 0; j < nch; ++j) pol[c4::kth_bit(legal, (int)j)] = (float)rec[1 + j];
+            const int idx = (int)(pick & 0xFFu), a = (int)((pick >> 8) & 0xFFu);
             c4::State cs;
-            c4::next_state(rs, a, cs);
+            SPAI_CHECK((uint32_t)idx < nch && a == c4::kth_bit(legal, idx) && c4::next_state(rs, a, cs) == 0 &&
+                           cs.status == ((pick >> 16) & 0xFFu),
+                       SPAI_ERR_INVALID, "internal: game %u's device move does not replay", t);
             const size_t m = ++h_len[t];   // plies so far, this one included
             SPAI_CHECK(m <= kPlies, SPAI_ERR_INVALID, "internal: game %u longer than %zu plies", t, kPlies);
             c4::State *hs = h_states.data() + (size_t)t * kPlies;
             float *hp = h_pol.data() + (size_t)t * kPlies * 7;
             int32_t *hm = h_moves.data() + (size_t)t * kPlies;
             hs[m - 1] = rs;
-            std::memcpy(hp + (m - 1) * 7, pol.data() + (size_t)k * 7, 7 * sizeof(float));
+            normalize_policy(pol, hp + (m - 1) * 7);
             hm[m - 1] = a;
             if (cs.status != c4::kOngoing) {                  // is_terminal: emit, trees_vec.remove(i)
                 const float v = c4::terminal_value(cs.status);
@@ -953,24 +1162,23 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
                 games += 1;
                 positions += (double)m;
                 h_len[t] = 0;
-                active[k] = kNoSlot;                          // removed below, order kept
-            } else {                                          // use_subtree(selected_id)
-                T.h_root[t] = T.h_root_first[t] + (uint32_t)idx;
+            } else {                                          // use_subtree(selected_id), already on the device
+                T.h_root[t] = first + (uint32_t)idx;
                 T.h_root_state[t] = cs;
                 T.h_root_nch[t] = 0;
             }
         }
-        active.erase(std::remove(active.begin(), active.end(), kNoSlot), active.end());
-        SPAI_TRY(upload_roots(e, 0, T.n_trees));
-        if (trace)   // move, active trees, leaves evaluated, search seconds, host seconds (sampling + root
-                     // upload), search passes (tail mode; 0: one launch pair per iteration)
-            std::fprintf(trace, "%llu,%u,%.0f,%.6f,%.6f,%u\n", (unsigned long long)move_no, na, ev,
+        if (trace)   // move, active trees, leaves evaluated, search seconds (launch to records), host seconds
+                     // between the records and the next launch, search passes (tail mode; 0: one launch pair
+                     // per iteration), bookkeeping seconds (overlapping the next search)
+            std::fprintf(trace, "%llu,%u,%.0f,%.6f,%.6f,%u,%.6f\n", (unsigned long long)move_no, na, ev,
                          std::chrono::duration<double>(tm1 - tm0).count(),
-                         std::chrono::duration<double>(std::chrono::steady_clock::now() - tm1).count(),
-                         e->last_tail_passes);
+                         std::chrono::duration<double>(tm2 - tm1).count(), passes,
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - tm3).count());
+        tm0 = tm2;
+        cur ^= 1;
         ++move_no;
     }
-    if (trace) std::fclose(trace);
     if (stats) {
         stats->sims = sims;
         stats->evals = evals;

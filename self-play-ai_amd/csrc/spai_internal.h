@@ -205,6 +205,14 @@ struct spai_engine {
     spai::DevBuf<uint32_t> active;   // active tree list
     spai::DevBuf<uint32_t> err;      // device error flags
     spai::DevBuf<uint32_t> stats;    // root stats [n][8]
+    // self-play's move step on the device (search.hip k_advance): visits^T for every
+    // visit count a game can reach (the host's std::pow), and the per-move records,
+    // read back into one of two pinned buffers (move m's is read while m + 1 runs)
+    spai::DevBuf<double> pow_tab;
+    double pow_tab_t = -1.0;
+    spai::DevBuf<uint32_t> move_out;
+    uint32_t *h_move[2] = {nullptr, nullptr};
+    size_t h_move_n = 0;
     spai::KernelTimer timer;
 };
 

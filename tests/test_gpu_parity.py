@@ -404,6 +404,31 @@ def test_self_play_hash_matches_oracle(spai, oracle):
     e.close()
 
 
+@pytest.mark.parametrize("temperature", [0.7, 3.0])
+def test_self_play_device_sampling_matches_oracle(spai, oracle, temperature):
+    """the move step on the device (search.hip k_advance: Philox uniform,
+    WeightedIndex over the std::pow table of visits^T, the new root written in
+    place): at temperatures other than the default, and for a second run on the
+    same engine (the table reused) at another game-id base, the sample stream is
+    the oracle's bit for bit"""
+    n, sims, seed = 72, 24, 5
+    e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_HASH, seed=seed, temperature=temperature)
+    for base in (0, 1000):
+        games, stats = e.self_play(n, game_id_base=base)
+        ref = oracle.self_play(oracle.GAME_CONNECT4, n, sims, seed, eval_kind=oracle.EVAL_HASH, max_plies=42,
+                               temperature=temperature, game_id_base=base)
+        k = 0
+        for g in games:   # (the oracle numbers its games from 0, the engine from the base)
+            m = len(g["value"])
+            assert [int(v) + base for v in ref["game"][k:k + m]] == [g["game"]] * m
+            np.testing.assert_array_equal(g["policy"], ref["policy"][k:k + m])
+            np.testing.assert_array_equal(g["value"], ref["value"][k:k + m])
+            np.testing.assert_array_equal(g["enc"], ref["enc"][k:k + m])
+            k += m
+        assert k == len(ref["value"]) and stats["sims"] == ref["sims"] and stats["games"] == n
+    e.close()
+
+
 kTailChunk = 4   # search.hip: passes per host check
 
 
