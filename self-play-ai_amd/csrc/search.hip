@@ -109,6 +109,12 @@ __device__ __forceinline__ void backup_store(uint4 *nodes, const uint32_t (&node
         }
     }
 }
+__device__ __forceinline__ void backup_nodes(uint4 *nodes, const uint32_t (&node)[kLevelsPerLane], int d, float v,
+                                             int lane8) {
+    uint2 r[kLevelsPerLane];
+    backup_load(nodes, node, d, lane8, r);
+    backup_store(nodes, node, d, v, lane8, r);
+}
 
 // this lane's bit of its tree's 8-lane group in a wave-wide ballot
 __device__ __forceinline__ uint32_t group_bits(uint64_t ball) {
@@ -133,7 +139,7 @@ __device__ __forceinline__ uint32_t score_key(float u) {
 // the child index in the key's low bits, and the child record's visit count and
 // children word (what the next level needs)
 struct Cand {
-    uint32_t hi, lo, n, w, y;
+    uint32_t hi, lo, n, w;
 };
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
@@ -142,14 +148,12 @@ __device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
 // one butterfly step: take the partner lane's candidate if its key is larger
 template <int CTRL>
 __device__ __forceinline__ void cand_step(Cand &c) {
-    const Cand o{dpp_mov<CTRL>(c.hi), dpp_mov<CTRL>(c.lo), dpp_mov<CTRL>(c.n), dpp_mov<CTRL>(c.w),
-                 dpp_mov<CTRL>(c.y)};
+    const Cand o{dpp_mov<CTRL>(c.hi), dpp_mov<CTRL>(c.lo), dpp_mov<CTRL>(c.n), dpp_mov<CTRL>(c.w)};
     const bool take = (((uint64_t)o.hi << 32) | o.lo) > (((uint64_t)c.hi << 32) | c.lo);
     c.hi = take ? o.hi : c.hi;
     c.lo = take ? o.lo : c.lo;
     c.n = take ? o.n : c.n;
     c.w = take ? o.w : c.w;
-    c.y = take ? o.y : c.y;
 }
 
 // a tree's root for this search call: node id and position (constant while it
@@ -161,12 +165,11 @@ struct RootInfo {
     uint64_t x, o;
     uint8_t n, status;
     uint32_t rn, rw;
-    uint32_t ry;   // the root's value sum (f32 bits), current in lane 0 (the lane that backs level 0 up)
 };
 __device__ __forceinline__ RootInfo load_root(const TreeView &T, uint32_t t) {
     const uint32_t node = T.root[t];
     const uint4 r = T.nodes[(size_t)t * T.cap + node];
-    return RootInfo{node, T.root_x[t], T.root_o[t], T.root_n[t], T.root_status[t], r.x, r.w, r.y};
+    return RootInfo{node, T.root_x[t], T.root_o[t], T.root_n[t], T.root_status[t], r.x, r.w};
 }
 
 // One PUCT descent of tree t (mcts.rs:235-250) by its 8 lanes.  A terminal leaf
@@ -182,7 +185,7 @@ __device__ __forceinline__ RootInfo load_root(const TreeView &T, uint32_t t) {
 // (score, column), carrying the child index, visit count and children word --
 // no lane shuffle through the LDS crossbar and no branch on the chain.
 enum Descent { kTerminal = 0, kLive = 1, kError = 2 };
-__device__ __forceinline__ Descent descend(const TreeView &T, uint32_t t, RootInfo &root, int lane8, float c,
+__device__ __forceinline__ Descent descend(const TreeView &T, uint32_t t, const RootInfo &root, int lane8, float c,
                                            uint32_t *err, uint64_t &x, uint64_t &o, uint8_t &n) {
     uint4 *nodes = T.nodes + (size_t)t * T.cap;
     uint32_t *path = T.path + (size_t)t * kMaxDepth;
@@ -192,12 +195,8 @@ __device__ __forceinline__ Descent descend(const TreeView &T, uint32_t t, RootIn
     n = root.n;
     uint8_t status = root.status;
     uint32_t rn = root.rn, rw = root.rw;   // the current node's visit count and children word
-    // path levels == lane8 (mod 8) kept in this lane's registers (kMaxDepth = 6 x 8):
-    // node id, and the visit count and value sum its record had when the descent
-    // read it (only this tree's lanes write its records, so they are current)
+    // path levels == lane8 (mod 8) kept in this lane's registers (kMaxDepth = 6 x 8)
     uint32_t pr[kLevelsPerLane] = {node, 0u, 0u, 0u, 0u, 0u};
-    uint32_t pn[kLevelsPerLane] = {rn, 0u, 0u, 0u, 0u, 0u};
-    uint32_t py[kLevelsPerLane] = {root.ry, 0u, 0u, 0u, 0u, 0u};
     const int top = 7 * lane8 + 5;   // this column's top cell (lane 7: none)
     int d = 0;
     if (lane8 == 0) path[0] = node;
@@ -209,7 +208,7 @@ __device__ __forceinline__ Descent descend(const TreeView &T, uint32_t t, RootIn
         const uint4 ch = nodes[first + (open ? k : 0u)];
         const float sq = sqrtf((float)rn);
         const float u = ucb(sq, ch, c);
-        Cand w{open ? score_key(u) : 0u, ((uint32_t)lane8 << 3) | k, ch.x, ch.w, ch.y};
+        Cand w{open ? score_key(u) : 0u, ((uint32_t)lane8 << 3) | k, ch.x, ch.w};
         cand_step<0xB1>(w);    // quad_perm [1,0,3,2]: lane ^ 1
         cand_step<0x4E>(w);    // quad_perm [2,3,0,1]: lane ^ 2
         cand_step<0x141>(w);   // row_half_mirror: lane i <-> 7 - i of the 8, across the two quads
@@ -241,26 +240,11 @@ __device__ __forceinline__ Descent descend(const TreeView &T, uint32_t t, RootIn
         const bool mine = (d & 7) == lane8;
         if (mine) path[d] = node;
 #pragma unroll
-        for (int j = 0; j < kLevelsPerLane; ++j) {
-            const bool here = mine && (d >> 3) == j;
-            pr[j] = here ? node : pr[j];
-            pn[j] = here ? w.n : pn[j];
-            py[j] = here ? w.y : py[j];
-        }
+        for (int j = 0; j < kLevelsPerLane; ++j) pr[j] = mine && (d >> 3) == j ? node : pr[j];
     }
     if (lane8 == 0) T.depth[t] = (uint8_t)d;
-    if (status != c4::kOngoing) {   // terminal leaf: backprop(leaf, value), mcts.rs:245-247
-        // from the records as the descent read them: stores only, no second round trip
-        const float v = c4::terminal_value(status);
-#pragma unroll
-        for (int j = 0; j < kLevelsPerLane; ++j) {
-            const int lvl = lane8 + 8 * j;
-            const float sign = ((d - lvl) & 1) ? -1.0f : 1.0f;
-            const uint32_t ny = __float_as_uint(__uint_as_float(py[j]) + sign * v);
-            if (lvl <= d) *(uint2 *)(nodes + pr[j]) = make_uint2(pn[j] + 1u, ny);
-            if (j == 0) root.ry = lane8 == 0 ? ny : root.ry;
-        }
-        root.rn += 1;   // the backup's visit of the root
+    if (status != c4::kOngoing) {                           // terminal leaf: backprop(leaf, value), mcts.rs:245-247
+        backup_nodes(nodes, pr, d, c4::terminal_value(status), lane8);
         return kTerminal;
     }
     return kLive;
@@ -311,6 +295,7 @@ __device__ __forceinline__ void select_tree(const TreeView &T, const BatchView &
         const Descent r = descend(T, t, root, lane8, c, err, x, o, n);
         if (r == kLive) slot_leaf(T, B, t, lane8, x, o, n);
         if (r != kTerminal) break;
+        root.rn += 1;   // the backup's visit of the root
         // the next descent reads records the other lanes of this tree just backed
         // up: one wave, so a wavefront-scope fence (as in k_expand_select)
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -373,7 +358,6 @@ __device__ __forceinline__ void expand_leaf(const TreeView &T, const BatchView &
     }
     backup_store(nodes, node, d, value, lane8, r);
     root.rn += 1;
-    if (lane8 == 0) root.ry = __float_as_uint(__uint_as_float(r[0].y) + ((d & 1) ? -1.0f : 1.0f) * value);
     if (d == 0) root.rw = first | (nch << 24);
 }
 
