@@ -760,10 +760,15 @@ int search_launch(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t
     const char *tt_env = std::getenv("SPAI_TAIL_TREE_EVALS");
     const double tail_leaves = tl_env ? std::atof(tl_env) : kTailLeaves;
     const uint32_t tail_tree = tt_env ? (uint32_t)std::max(0, std::atoi(tt_env)) : kTailTreeEvals;
-    const char *tr_env = std::getenv("SPAI_TAIL_RUN");
-    const uint32_t tail_run = tr_env ? (uint32_t)std::max(1, std::atoi(tr_env)) : kTailRun;
     const bool tail = num_searches > 0 && e->last_evals_per_iter >= 0 &&
                       (e->last_evals_per_iter < tail_leaves || e->last_max_tree_evals < tail_tree);
+    // the run cap; after a call that evaluated nothing (every tree solved: no tree
+    // to keep waiting) none, and a check after every pass -- normally one
+    const bool solved = e->last_evals_per_iter == 0.0;
+    const char *tr_env = std::getenv("SPAI_TAIL_RUN");
+    const uint32_t tail_run =
+        tr_env ? (uint32_t)std::max(1, std::atoi(tr_env)) : (solved ? std::max(num_searches, 1u) : kTailRun);
+    const uint32_t tail_chunk = solved ? 1u : kTailChunk;
     // chain h searches active[off[h] .. off[h] + cnt[h]) on chain_stream[h]
     const ChainPolicy pol = tail ? ChainPolicy{1, 0u} : chains_for(n, e->last_evals_per_iter);
     const int nchain = pol.chains;
@@ -805,14 +810,14 @@ int search_launch(spai_engine *e, uint32_t n, const uint32_t *tree_idx, uint32_t
         // terminal leaves (at most tail_run per pass).  A pass whose select slots
         // no leaf and caps no tree leaves no tree with iterations to run (a tree
         // stops a launch only at a live leaf or the cap), so the host checks every
-        // kTailChunk passes and stops there.
+        // tail_chunk passes and stops there.
         const uint32_t g8 = (n + kTreesPerBlock - 1) / kTreesPerBlock;
         const uint32_t *act = e->active.p;
         k_set_left<<<(n + 255) / 256, 256, 0, st>>>(tv, act, n, num_searches);
         k_select<true><<<g8, kBlock, 0, st>>>(tv, batch_view(e, 0, 0), act, n, e->cfg.c, e->err.p, tail_run);
         uint32_t p = 0, next = 1, more = 0;
         for (;;) {
-            for (uint32_t q = 0; q < kTailChunk; ++q, ++p) {
+            for (uint32_t q = 0; q < tail_chunk; ++q, ++p) {
                 const BatchView bv = batch_view(e, 0, p);
                 if (kind == SPAI_EVAL_NET) {
                     SPAI_TRY(net_eval_batch(e->net, st, bv.count, n, bv.mine, bv.theirs, bv.priors, bv.value, 0));
