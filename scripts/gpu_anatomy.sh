@@ -1,5 +1,5 @@
 # Anatomy of one C4 bench step: rocprofv3 kernel trace of bench.py (1 step, no
-# warm-up) cut into moves at k_root_stats (scripts/step_anatomy.py), plus the
+# warm-up) cut into moves at k_advance (k_root_stats before it; scripts/step_anatomy.py), plus the
 # per-move host trace.  ENV_AB="VAR=val ..." runs a second traced step with those
 # environment settings for comparison.
 set -o pipefail
