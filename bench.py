@@ -7,10 +7,17 @@ simulations per move against a random-init 6-block x 64 ResNet (bf16 MFMA),
 all of it on the device (search trees in HBM, fused net forward per search
 iteration).  value = MCTS simulations per second summed over all ranks.
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): games are
-sharded by id across ranks (rank r plays ids [r*G, (r+1)*G) per step), no
-collective touches the data path; a rank-0 TCP star (hostgroup.py, not torch
-gloo) carries only the timing barrier and the max/sum reductions.  The GPU
+Multi-GPU: `python bench.py --gpus N` (no launcher) starts N rank processes
+itself, one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N, MASTER_* on
+127.0.0.1), and relays rank 0's line; under `torch.distributed.run
+--nproc-per-node N ... bench.py --gpus N` the launcher's ranks are used and
+WORLD_SIZE must equal N.  Games are sharded by id across ranks (rank r plays
+ids [r*G, (r+1)*G) per step), no collective touches the data path (main.rs:
+169-186,220-234: each worker owns its Mcts + Model); a rank-0 TCP star
+(hostgroup.py, not torch gloo) carries the timing barrier and the max/sum
+reductions, and the same work counters and step times are reduced once more
+through an N-rank RCCL communicator over the ranks' devices (`rccl` in the
+line: its rank count and whether its sums equal the host group's).  The GPU
 process never imports torch (torch ships its own HIP runtime with the same
 SONAME).
 
@@ -81,7 +88,7 @@ def parse():
     ap.add_argument("--chess-moves", type=int, default=2)
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events (A/B of their cost)")
     ap.add_argument("--no-isolated", action="store_true", help="skip the isolated-forward measurement")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r04", "final", "forward_traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r04", "final_b", "forward_traffic.json"),
                     help="PMC summary (scripts/gpu_traffic.sh) of this bench command: HBM bytes per k_forward launch")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
@@ -237,11 +244,76 @@ def chess_window(args, device):
             "kernel_ms": {"select_leaf": ms[0], "forward": ms[1], "expand": ms[2]}}
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this same
+    command (rank r on GPU r), rank 0's stdout to ours, the others' to our stderr.
+    This process never imports the library or touches a GPU.  If a rank fails the
+    others are stopped (a rank blocked in a barrier would otherwise wait forever).
+    Returns the worst exit status."""
+    port, group_port = _free_port(), _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SPAI_GROUP_PORT=str(group_port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    rcs = [None] * n
+    try:
+        while any(rc is None for rc in rcs):
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    rcs[r] = p.poll()
+            if any(rc not in (None, 0) for rc in rcs):
+                break
+            time.sleep(0.2)
+    finally:
+        own = list(rcs)   # exit statuses the ranks reached on their own
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                p.terminate()
+                try:
+                    rcs[r] = p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    rcs[r] = p.wait()
+    if all(rc == 0 for rc in rcs):
+        return 0
+    print("bench.py: rank exit status %s" % rcs, file=sys.stderr)
+    failed = [rc for rc in own if rc not in (None, 0)]
+    return failed[0] if failed and failed[0] > 0 else 1
+
+
+def rccl_comm(dist, spai):
+    """an RCCL communicator over the ranks' devices (rank 0's id through the host
+    group); None with a reason when the ranks share a device (RCCL refuses that)"""
+    devs = dist.g.allgather(dist.local)
+    if len(set(devs)) != len(devs):
+        return None, "ranks share device(s) %s: RCCL needs one rank per GPU; host group only" % devs
+    uid = dist.g.broadcast_bytes(spai.comm_unique_id() if dist.rank == 0 else None)
+    try:
+        return spai.Comm(dist.local, dist.rank, dist.world, uid), None
+    except Exception as ex:   # reported in the line; the host group still carries the reductions
+        return None, "RCCL communicator failed: %r" % (ex,)
+
+
 def main():
     args = parse()
     if args.cpu_baseline_only:
         cpu_baseline(args)
         return
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            sys.exit(spawn_ranks(args.gpus))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit("bench.py: --gpus %d but the launcher started WORLD_SIZE=%s ranks"
+                 % (args.gpus, os.environ["WORLD_SIZE"]))
     dist = Dist()
     import spai
 
@@ -249,6 +321,7 @@ def main():
                       seed=args.seed)
     net = spai.Net(eng, args.blocks, spai.init_params(args.blocks, 64, seed=args.seed))
     eng.set_net(net)
+    comm, comm_note = rccl_comm(dist, spai)
     G = args.games
 
     def step(i):
@@ -274,7 +347,18 @@ def main():
     dt = time.perf_counter() - t0
     timing = eng.timing()
     (dt_max,) = dist.reduce([dt], "max")
-    sims, games, evals, positions = dist.reduce([tot["sims"], tot["games"], tot["evals"], tot["positions"]], "sum")
+    counters = [tot["sims"], tot["games"], tot["evals"], tot["positions"]]
+    sims, games, evals, positions = dist.reduce(counters, "sum")
+    rccl = {"ranks": 0, "note": comm_note}
+    if comm is not None:   # the same reductions over RCCL (xGMI between GPUs): exact for these integer counts
+        try:
+            r_sum = comm.allreduce(counters, "sum")
+            (r_max,) = comm.allreduce([dt], "max")
+            rccl = {"ranks": comm.info()[1], "devices": dist.g.allgather(dist.local),
+                    "counters_agree": r_sum == [sims, games, evals, positions] and r_max == dt_max}
+        except Exception as ex:
+            rccl = {"ranks": 0, "note": "RCCL all-reduce failed: %r" % (ex,)}
+        comm.close()
 
     fpe = flops_per_eval(args.blocks)
     ev = timing["evaluate"]
@@ -308,6 +392,8 @@ def main():
                    "model": "c4-resnet-%dx64" % args.blocks, "games_per_gpu": G, "sims_per_move": args.sims,
                    "global_batch": G * dist.world, "parallelism": "dp%d (games sharded, no collective)" % dist.world},
         "work": {"sims": sims, "games": games, "evals": evals, "positions": positions},   # summed over ranks
+        "rccl_ranks": rccl["ranks"],
+        "rccl": rccl,
         "evals_per_sec": evals / dt_max,
         "positions_per_sec": positions / dt_max,
         "kernel_ms": {k: v["avg_ms"] for k, v in timing.items()},
@@ -357,8 +443,6 @@ def main():
             result["chess"] = chess_window(args, dist.local)
         except Exception as ex:   # the window must never sink the headline number
             result["chess"] = {"error": repr(ex)[:300]}
-    net.close()
-    eng.close()
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         cb = run_cpu_baseline(args)
         result["cpu_baseline"] = cb

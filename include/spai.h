@@ -272,6 +272,20 @@ int spai_learner_activation(spai_learner *l, int layer, float *out, size_t n);
  * copy); world 1 with NULL drops the communicator. */
 int spai_comm_unique_id(uint8_t *id /* SPAI_COMM_ID_BYTES */);
 int spai_learner_set_comm(spai_learner *l, int rank, int world, const uint8_t *id);
+/* A stand-alone RCCL communicator, one rank per GPU (comm.cpp).  The worker
+ * fan-out it sits beside (main.rs:169-186,220-234) has no collective: the
+ * sharded self-play bench reduces its per-rank work counters and step times
+ * through it once per run, so an N-GPU run shows RCCL formed N ranks over
+ * xGMI.  RCCL refuses two ranks on one device: such ranks use the host group.
+ * spai_comm_allreduce_f64 reduces n host doubles in place (H2D, ncclAllReduce,
+ * D2H on the communicator's stream; blocks until every rank has arrived). */
+typedef struct spai_comm spai_comm;
+enum { SPAI_REDUCE_SUM = 0, SPAI_REDUCE_MAX = 1 };
+int spai_comm_create(int device, int rank, int world, const uint8_t *id /* SPAI_COMM_ID_BYTES */,
+                     spai_comm **out);
+int spai_comm_allreduce_f64(spai_comm *c, double *buf, size_t n, int op /* SPAI_REDUCE_* */);
+int spai_comm_info(spai_comm *c, int *rank, int *world, int *device);
+int spai_comm_destroy(spai_comm *c);
 /* Weight refresh for self-play replicas (learner_concurrent.rs:158-159,260-264 hands the
  * trainer's weights to the self-play workers): RCCL broadcast of rank `root`'s parameters
  * to every rank of the communicator; a learner without one is left unchanged. */

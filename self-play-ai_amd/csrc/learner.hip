@@ -1203,11 +1203,15 @@ int learner_set_host_comm(spai_learner *L, int rank, int world, spai_host_allred
         (void)ncclCommDestroy((ncclComm_t)L->comm);
         L->comm = nullptr;
     }
-    L->rank = fn ? rank : 0;
-    L->world = fn ? world : 1;
-    L->host_ar = fn;
-    L->host_ar_user = user;
-    if (!fn) return SPAI_OK;
+    // NULL or world 1 drops the collective (spai.h): a 1-rank reduction is the
+    // identity, and staging it through host memory would cost the step its
+    // launch-only property (three syncs and callbacks per step)
+    const bool on = fn && world > 1;
+    L->rank = on ? rank : 0;
+    L->world = on ? world : 1;
+    L->host_ar = on ? fn : nullptr;
+    L->host_ar_user = on ? user : nullptr;
+    if (!on) return SPAI_OK;
     const size_t need = std::max(L->n_params, L->run_idx.n);
     if (L->host_buf_n < need) {
         if (L->host_buf) (void)hipHostFree(L->host_buf);

@@ -590,7 +590,11 @@ ChainPolicy chains_for(uint32_t n, double last_evals_per_iter) {
     static const int mid_chains = std::max(1, std::min(spai_engine::kChains, env_int("SPAI_MID_CHAINS", 2)));
     static const uint32_t mid_grid = (uint32_t)std::max(0, env_int("SPAI_MID_GRID", 0));
     static const double min_chain_leaves = env_int("SPAI_MIN_CHAIN_LEAVES", (int)kMinChainLeaves);   // A/B knob
+    // A/B knob: one chain at or above this many leaves per iteration (a fresh set
+    // of trees counts as one leaf per tree)
+    static const int hi_leaves = env_int("SPAI_HI_LEAVES", 0);
     if (forced) return {std::max(1, std::min<int>(forced, (int)(n / 64))), 0u};
+    if (hi_leaves > 0 && (last_evals_per_iter < 0 ? (double)n : last_evals_per_iter) >= hi_leaves) return {1, 0u};
     if (last_evals_per_iter >= 0 && last_evals_per_iter < min_chain_leaves) return {1, 0u};
     if (last_evals_per_iter >= 0 && last_evals_per_iter < mid_leaves)
         return {std::max(1, std::min<int>(mid_chains, (int)(n / 64))), mid_grid};
@@ -1082,6 +1086,17 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
         SPAI_HIP(hipMemcpyAsync(dst, e->move_out.p, words * 4, hipMemcpyDeviceToHost, st));
         return SPAI_OK;
     };
+    // every return below, errors included, leaves the engine quiescent: the next
+    // move's search, k_advance and the record copy may be in flight when a
+    // bookkeeping check fails (they write device roots and a pinned buffer)
+    struct Quiesce {
+        spai_engine *e;
+        ~Quiesce() {
+            (void)hipStreamSynchronize(e->stream);
+            for (hipStream_t cs : e->chain_stream)
+                if (cs) (void)hipStreamSynchronize(cs);
+        }
+    } quiesce{e};
     uint64_t move_no = 0;
     int cur = 0;
     auto tm0 = std::chrono::steady_clock::now();

@@ -28,7 +28,12 @@ class Config3Rank:
     def __init__(self, rank, world, uid, games=4096, sims=800, blocks=6, batch=128, train_steps=20, fraction=0.3,
                  capacity=None, seed=0, device=0, group=None):
         self.rank, self.world = rank, world
-        self.group = group   # host group (hostgroup.HostGroup): agrees the step count over ranks
+        # host group (hostgroup.HostGroup): agrees the step count over ranks.  Every
+        # train step is a collective, so ranks that counted their own ring sizes
+        # could issue different numbers of them and hang: required when world > 1
+        if world > 1 and group is None:
+            raise ValueError("Config3Rank: world %d needs a host group to agree the train steps" % world)
+        self.group = group
         self.games, self.sims, self.blocks = games, sims, blocks
         self.batch, self.train_steps, self.fraction, self.seed = batch, train_steps, fraction, seed
         self.eng = spai.Engine(num_searches=sims, max_trees=games, eval_kind=spai.EVAL_NET, device=device, seed=seed)

@@ -36,6 +36,7 @@ SYMBOLS = [
     "spai_net_phase_cycles", "spai_net_bench", "spai_adam_config_default", "spai_learner_create", "spai_learner_destroy",
     "spai_learner_train_batch", "spai_learner_params", "spai_learner_grads", "spai_learner_activation", "spai_comm_unique_id",
     "spai_learner_set_comm", "spai_learner_broadcast", "spai_learner_set_host_comm", "spai_learner_last_batch",
+    "spai_comm_create", "spai_comm_allreduce_f64", "spai_comm_info", "spai_comm_destroy",
     "spai_params_save_safetensors", "spai_params_load_safetensors",
     "spai_replay_create", "spai_replay_destroy", "spai_replay_push", "spai_replay_pop", "spai_replay_size",
     "spai_choose_multiple", "spai_pipeline_config_default", "spai_pipeline_run", "spai_learner_train",
@@ -179,6 +180,10 @@ def lib():
         L.spai_learner_broadcast.argtypes = [vp, i32]
         L.spai_learner_set_host_comm.argtypes = [vp, i32, i32, HOST_ALLREDUCE, vp]
         L.spai_learner_last_batch.argtypes = [vp, P(u32)]
+        L.spai_comm_create.argtypes = [i32, i32, i32, vp, P(vp)]
+        L.spai_comm_allreduce_f64.argtypes = [vp, vp, C.c_size_t, i32]
+        L.spai_comm_info.argtypes = [vp, P(i32), P(i32), P(i32)]
+        L.spai_comm_destroy.argtypes = [vp]
         L.spai_params_save_safetensors.argtypes = [i32, i32, i32, vp, C.c_size_t, C.c_char_p]
         L.spai_params_load_safetensors.argtypes = [i32, i32, i32, C.c_char_p, vp, C.c_size_t]
         L.spai_replay_create.argtypes = [u32, P(vp)]
@@ -533,6 +538,35 @@ def comm_unique_id():
     buf = np.zeros(COMM_ID_BYTES, np.uint8)
     _check(lib().spai_comm_unique_id(_p(buf)))
     return buf.tobytes()
+
+
+REDUCE_SUM, REDUCE_MAX = 0, 1
+
+
+class Comm:
+    """stand-alone RCCL communicator, one rank per GPU (spai_comm_*): rank 0 makes
+    the id (comm_unique_id), the host group hands it to the other ranks"""
+
+    def __init__(self, device, rank, world, uid):
+        buf = np.frombuffer(bytes(uid), np.uint8).copy()
+        self.h = C.c_void_p()
+        _check(lib().spai_comm_create(device, rank, world, _p(buf), C.byref(self.h)))
+
+    def info(self):
+        r, w, d = C.c_int(), C.c_int(), C.c_int()
+        _check(lib().spai_comm_info(self.h, C.byref(r), C.byref(w), C.byref(d)))
+        return r.value, w.value, d.value
+
+    def allreduce(self, values, op="sum"):
+        """list of floats reduced over the ranks (float64 ncclAllReduce)"""
+        a = np.ascontiguousarray(values, np.float64).copy()
+        _check(lib().spai_comm_allreduce_f64(self.h, _p(a), len(a), REDUCE_MAX if op == "max" else REDUCE_SUM))
+        return [float(v) for v in a]
+
+    def close(self):
+        if self.h:
+            lib().spai_comm_destroy(self.h)
+            self.h = C.c_void_p()
 
 
 def save_params(path, params, blocks, hidden=64, game=GAME_CONNECT4):

@@ -154,3 +154,38 @@ def test_bench_two_ranks_one_gpu(tmp_path):
     for k in ("sims", "evals", "games", "positions"):
         assert two["work"][k] == one["work"][k], (k, one["work"], two["work"])
     assert two["work"]["games"] == 2 * G
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    """`python bench.py --gpus 2` exactly as the driver invokes the 1-GPU bench (no
+    launcher, no RANK / WORLD_SIZE in the environment): bench.py starts the two
+    rank processes itself.  Both share device 0 here (SPAI_BENCH_DEVICE=0), so
+    RCCL (one rank per GPU) is skipped with a reason and the host group carries
+    the reductions; the line says n_gpus 2 and its work equals one rank's 2G
+    games.  The 1-rank run forms a 1-rank RCCL communicator whose sums must equal
+    the host group's (main.rs:169-186,220-234)"""
+    import json
+    import subprocess
+    import sys
+    from conftest import REPO
+    G = 96
+    args = ["--sims", "32", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-isolated",
+            "--no-rules-bench", "--no-chess", "--no-timing"]
+    env = dict(os.environ, SPAI_BENCH_DEVICE="0")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+
+    def run(gpus, games):
+        p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(gpus),
+                            "--games", str(games)] + args, env=env, capture_output=True, text=True, timeout=240)
+        assert p.returncode == 0, p.stderr[-3000:]
+        lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+        assert len(lines) == 1, p.stdout[-2000:]   # rank 0's line only
+        return json.loads(lines[0])
+
+    one, two = run(1, 2 * G), run(2, G)
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2 and two["config"]["global_batch"] == 2 * G
+    for k in ("sims", "evals", "games", "positions"):
+        assert two["work"][k] == one["work"][k], (k, one["work"], two["work"])
+    assert one["rccl_ranks"] == 1 and one["rccl"]["counters_agree"] is True, one["rccl"]
+    assert two["rccl_ranks"] == 0 and "share" in two["rccl"]["note"], two["rccl"]

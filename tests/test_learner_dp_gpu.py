@@ -284,3 +284,31 @@ def test_learner_last_batch_after_train(spai):
     assert a.shape == (70 % 32, 64, 6, 7) and (a >= 0).all() and (a > 0).any()
     L.close()
     e.close()
+
+
+def test_host_comm_world_one_is_dropped(spai):
+    """spai.h: a host collective with world 1 (or a NULL fn) is dropped, so the
+    step stays launch-only: the function is never called and the step equals a
+    plain learner's bit for bit"""
+    blocks = 1
+    p0 = spai.init_params(blocks, 64, seed=5)
+    (step,) = _batches(spai, [32], 1, seed=11)
+    calls = []
+
+    def fn(buf):
+        calls.append(len(buf))
+
+    eng = [spai.Engine(num_searches=1, max_trees=1) for _ in range(2)]
+    La, Lb = spai.Learner(eng[0], blocks, p0), spai.Learner(eng[1], blocks, p0)
+    try:
+        La.set_host_comm(0, 1, fn)
+        la, lb = La.train_batch(*step[0]), Lb.train_batch(*step[0])
+        La.broadcast(0)
+        assert calls == []
+        assert np.array_equal(np.asarray(la), np.asarray(lb))
+        assert np.array_equal(La.params(), Lb.params())
+    finally:
+        La.close()
+        Lb.close()
+        for e in eng:
+            e.close()
