@@ -44,8 +44,20 @@ constexpr int kS = 8;                      // max positions per workgroup group
 constexpr int kP = kS * c4::kCells;        // 336 board cells (LDS rows) at S = 8
 // position tiles (16 LDS rows each) for a group of S positions
 __host__ __device__ constexpr int npt_of(int S) { return (S * c4::kCells + 15) / 16; }
-constexpr int kWaves = 4;
-constexpr int kThreads = kWaves * 64;
+constexpr int kWaves = 4;                  // plan waves: the work split of every layer
+// SPAI_W8 (experimental build): two waves per SIMD.  Waves W and W + 4 run plan
+// wave W's tasks of every trunk conv over the two halves of K (the k-steps of
+// input channels 0-31 and 32-63 of each tap: the same weight bytes per CU, half
+// each), exchange half their partial sums through LDS and each finishes half
+// the tasks; the stem, head and linear run on waves 0-3.  Group sizes <= 5 only
+// (the partial-sum buffer must fit beside the activations).
+#ifdef SPAI_W8
+constexpr int kPhysWaves = 8;
+#else
+constexpr int kPhysWaves = 4;
+#endif
+constexpr int kThreads = kPhysWaves * 64;
+constexpr int kStemThreads = kWaves * 64;   // the per-position setup work (stem weights, planes)
 constexpr int kKStepsRes = 18;             // 576 / 32
 constexpr int kHeadC = 35;                 // 32 policy + 3 value channels
 constexpr int kPolIn = 32 * c4::kCells;    // 1344
@@ -79,7 +91,7 @@ constexpr int kL = kB + kS * 16;           // linear partials [4 waves][halves][
 constexpr int kMaxBlocks = 20;
 constexpr int kBiasFloats = kHid + 2 * kMaxBlocks * kHid + kHid;   // stem, residual convs, head (64 padded)
 constexpr int kBias = kL + kWaves * kLinHalves * 64 * 4; // all conv biases, staged once per workgroup
-constexpr int kBiasPer = (kBiasFloats + kThreads - 1) / kThreads;   // per thread
+constexpr int kBiasPer = (kBiasFloats + kStemThreads - 1) / kStemThreads;   // per thread
 constexpr int kPlanes = kBias + kBiasFloats * 4;   // stem neighbour planes [8][34] u64 (272-B rows: positions
                                                    // in different 16-B bank groups)
 constexpr int kPlaneRow = 34;
@@ -89,7 +101,15 @@ constexpr int kTab = kWStem + 4 * 64 * 16;         // k_geo_init: one S's row-gr
 // registers at the head conv's start (an LDS-DMA copy made the compiler wait
 // vmcnt(0) at the head k-loop's first weight use).
 constexpr int kLinWPer = kLinBSteps / kWaves;      // B fragments per wave
+#ifdef SPAI_W8
+constexpr int kSRun = 5;                   // largest group size this build runs
+constexpr int kSplitMaxN = 14;             // most tasks of a plan wave at S <= kSRun (S = 5, position-major)
+constexpr int kPart = kTab + 42 * 16;      // split-K partial sums [4 plan waves][kSplitMaxN][64 lanes] x 16 B
+constexpr int kLdsBytes = kPart + kWaves * kSplitMaxN * 1024;
+#else
+constexpr int kSRun = kS;
 constexpr int kLdsBytes = kTab + 42 * 16;
+#endif
 constexpr int kStamps = 24;                // phase stamps per wave in the diagnostic mode (17..19: inside block 0 conv1;
                                            // 20/21: s_memtime / s_memrealtime at kernel entry, 22: s_memrealtime at the
                                            // first group's stamp 0, 23: s_memrealtime after the last group)
@@ -130,13 +150,13 @@ constexpr bool kDiagEntry = true;
 #endif
 __device__ __forceinline__ void stamp(const NetParams &P, int wave, int lane, int k) {
 #ifdef SPAI_DIAG
-    if (P.stamps && lane == 0) P.stamps[((size_t)blockIdx.x * kWaves + wave) * kStamps + k] = __builtin_amdgcn_s_memtime();
+    if (P.stamps && lane == 0 && wave >= 0) P.stamps[((size_t)blockIdx.x * kWaves + wave) * kStamps + k] = __builtin_amdgcn_s_memtime();
 #endif
 }
 // wall-clock stamp (100 MHz constant clock), diagnostic build only
 __device__ __forceinline__ void stamp_real(const NetParams &P, int wave, int lane, int k) {
 #ifdef SPAI_DIAG
-    if (P.stamps && lane == 0)
+    if (P.stamps && lane == 0 && wave >= 0)
         P.stamps[((size_t)blockIdx.x * kWaves + wave) * kStamps + k] = __builtin_amdgcn_s_memrealtime();
 #endif
 }
@@ -835,7 +855,136 @@ __device__ __forceinline__ void linear_mfma(uint8_t *smem, int lane, const uint4
     }
 }
 
-template <int W, int S, bool FROM_X>
+
+// ---------------------------------------------------------------- split-K trunk conv (SPAI_W8)
+// Plan wave W's tasks over half of K: KH = 1 the k-steps of input channels 0-31
+// of every tap (even k-steps), KH = 2 those of channels 32-63 (odd).  The A
+// ring runs over the wave's 9 local k-steps (DA | 9) and carries the next
+// layer's first ones across the boundary.  Then the two waves of the pair swap
+// partial sums through LDS: each finishes half of the tasks as
+// (first-half sum incl. bias) + (second-half sum), adds the residual by the
+// identity MFMA (EPI = 2) and stores relu/bf16 to OUT.
+template <int W, int NPT>
+__device__ __forceinline__ int split_keep_lo() {
+    return (Plan<W, 4, NPT>::n + 1) / 2;   // tasks [0, h) finish on the KH = 1 wave, [h, n) on the KH = 2 wave
+}
+template <int W, int NPT, int S, int IN, int DA, int DB, int EPI, int OUT, int KH>
+__device__ __forceinline__ void conv_split(uint8_t *smem, const Geo<Plan<W, 4, NPT>::NT> &g, const float *bias,
+                                           const uint4 *__restrict__ w, const uint4 *__restrict__ wn, int lane,
+                                           uint4 (&A)[DA][Plan<W, 4, NPT>::CTL], f32x4 (&acc)[Plan<W, 4, NPT>::n]) {
+#ifdef SPAI_W8
+    using PL = Plan<W, 4, NPT>;
+    constexpr int NT = PL::NT, CTL = PL::CTL, n = PL::n, KL = kKStepsRes / 2, par = KH - 1;
+    static_assert(KH == 1 || KH == 2, "split half");
+    static_assert(KL % DA == 0, "the carried A ring needs DA | local k-steps");
+    static_assert(n <= kSplitMaxN, "partial-sum buffer");
+    const int q = lane >> 4;
+    f32x4 bv[CTL];
+#pragma unroll
+    for (int c = 0; c < CTL; ++c) {
+        if (KH == 1) {
+            const float4 b = *(const float4 *)(bias + (PL::C0 + c) * 16 + 4 * q);
+            bv[c] = f32x4{b.x, b.y, b.z, b.w};
+        } else {
+            bv[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+    const uint4 *wl = w + PL::C0 * 64 + lane;
+    const uint4 *wnl = wn + PL::C0 * 64 + lane;
+    auto live = [](int t, int j) { return !((tap_skip(S, PL::gpt(t)) >> j) & 1); };   // local step j = tap j
+    constexpr int la = DA - 1, lb = DB - 1;
+    uint4 B[DB][NT];
+#pragma unroll
+    for (int j = 0; j < lb; ++j)
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            if (live(t, j)) B[j][t] = *(const uint4 *)(smem + (IN - 256) + (g.b(t, j) ^ (par << 6)));
+    auto load_a = [&](int j) {
+        const int jj = j + la;
+#pragma unroll
+        for (int c = 0; c < CTL; ++c)
+            A[jj % DA][c] = jj < KL ? wl[((2 * jj + par) * 4 + c) * 64] : wnl[((2 * (jj - KL) + par) * 4 + c) * 64];
+    };
+#pragma unroll
+    for (int j = 0; j < KL; ++j) {
+        load_a(j);
+        int nr = 0;
+        if (j + lb < KL) {
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+                if (live(t, j + lb)) {
+                    B[(j + lb) % DB][t] = *(const uint4 *)(smem + (IN - 256) + (g.b(t, j + lb) ^ (par << 6)));
+                    ++nr;
+                }
+        }
+        int nm = 0;
+#pragma unroll
+        for (int i = 0; i < n; ++i)
+            if (live(PL::pt(i), j)) {
+                const int t = PL::gpt(PL::pt(i));
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[j % DA][PL::co(i) - PL::C0]),
+                                                                as_bf16x8(B[j % DB][PL::pt(i)]),
+                                                                2 * j == first_kstep(S, t) ? bv[PL::co(i) - PL::C0]
+                                                                                           : acc[i], 0, 0, 0);
+                ++nm;
+            }
+        const int ng = nm > nr ? nm : nr;
+#pragma unroll
+        for (int i = 0; i < n; ++i) {
+            if (i < ng) {
+                if (i < nm) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                if (i < nr) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                if (i < CTL) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    // swap half of the partial sums with the partner wave
+    constexpr int h = (n + 1) / 2;
+    constexpr int g0 = KH == 1 ? h : 0, g1 = KH == 1 ? n : h;   // given away
+    constexpr int k0 = KH == 1 ? 0 : h, k1 = KH == 1 ? h : n;   // kept and finished here
+    f32x4 *part = (f32x4 *)(smem + kPart) + (size_t)W * kSplitMaxN * 64 + lane;
+#pragma unroll
+    for (int i = g0; i < g1; ++i) part[i * 64] = acc[i];
+    __syncthreads();
+    uint4 id[2];
+    if (EPI == 2) {
+        const int m = lane & 15;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int jj = 16 * hh + m - 8 * q;
+            uint32_t wv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) wv[e] = jj == 2 * e ? 0x3F80u : jj == 2 * e + 1 ? 0x3F800000u : 0u;
+            id[hh] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        }
+    }
+#pragma unroll
+    for (int i = k0; i < k1; ++i) {
+        const f32x4 p = part[i * 64];
+        f32x4 a = KH == 1 ? acc[i] + p : p + acc[i];   // (first K half) + (second K half)
+        if (EPI == 2) {
+            const uint4 rb = *(const uint4 *)(smem + (OUT - 256) + (g.b(PL::pt(i), 4) ^ ((PL::co(i) >> 1) << 6)));
+            a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(id[PL::co(i) & 1]), as_bf16x8(rb), a, 0, 0, 0);
+        }
+        const int off = OUT + (g.epi[PL::pt(i)] ^ (PL::co(i) << 5));
+        *(uint2 *)(smem + off) = make_uint2(pack_relu_bf16x2(a[0], a[1]), pack_relu_bf16x2(a[2], a[3]));
+    }
+#else
+    (void)smem, (void)g, (void)bias, (void)w, (void)wn, (void)lane, (void)A, (void)acc;
+#endif
+}
+
+template <int KH, int CTL, int C0, int DA>
+__device__ __forceinline__ void load_a_first_split(const uint4 *__restrict__ w, int lane, uint4 (&A)[DA][CTL]) {
+#pragma unroll
+    for (int j = 0; j < DA - 1; ++j)
+#pragma unroll
+        for (int c = 0; c < CTL; ++c) A[j][c] = w[((2 * j + KH - 1) * 4 + C0 + c) * 64 + lane];
+}
+
+template <int W, int S, bool FROM_X, int KH>
 __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &P, const float *__restrict__ x,
                                                 int base, int valid, int lane, const Geo<Plan<W, 4, npt_of(S)>::NT> &g,
                                                 const int (&aux)[Plan<W, 4, npt_of(S)>::NT]) {
@@ -843,6 +992,38 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
     using PL4 = Plan<W, 4, NPT>;
     constexpr size_t kLayer = (size_t)kKStepsRes * 4 * 64;
     const float *bias = (const float *)(smem + kBias);
+    if constexpr (KH > 0) {   // SPAI_W8: split-K trunk on 8 waves, stem / head / linear on waves 0-3
+        constexpr int DA = 3, DB = b_depth(S), SW = KH == 2 ? -1 : W;
+        uint4 A[DA][PL4::CTL];
+        if (P.blocks > 0) load_a_first_split<KH, PL4::CTL, PL4::C0, DA>(P.w_res, lane, A);
+        if (KH == 1) stem<W, S, FROM_X>(smem, P, x, base, valid, lane, g, aux);
+        __syncthreads();
+        stamp(P, SW, lane, 1);
+        for (int b = 0; b < P.blocks; ++b) {
+            f32x4 acc[PL4::n];
+            const int l1 = 2 * b, l2 = 2 * b + 1;
+            conv_split<W, NPT, S, kX, DA, DB, 1, kY, KH>(smem, g, bias + kHid * (1 + l1), P.w_res + l1 * kLayer,
+                                                        P.w_res + l2 * kLayer, lane, A, acc);
+            layer_barrier();
+            if (l1 < 12) stamp(P, SW, lane, 2 + l1);
+            conv_split<W, NPT, S, kY, DA, DB, 2, kX, KH>(smem, g, bias + kHid * (1 + l2), P.w_res + l2 * kLayer,
+                                                        b + 1 < P.blocks ? P.w_res + (l2 + 1) * kLayer : P.w_res + l2 * kLayer,
+                                                        lane, A, acc);
+            layer_barrier();
+            if (l2 < 12) stamp(P, SW, lane, 2 + l2);
+        }
+        uint4 wlin[kLinWPer];
+        if (KH == 1) {
+            constexpr int DH = a_depth(S);
+            uint4 Ah[DH][PL4::CTL];
+            load_a_first<4, PL4::C0, PL4::CTL, DH>(P.w_head, lane, Ah);
+            head_layer<W, S, DH>(smem, P, lane, g, aux, Ah, wlin);
+        }
+        __syncthreads();
+        stamp(P, SW, lane, 14);
+        if (KH == 1) linear_mfma<W, S>(smem, lane, wlin);
+        return;
+    }
     constexpr int DA = a_depth(S), DB = b_depth(S);
     uint4 A[DA][PL4::CTL];
     load_a_first<4, PL4::C0, PL4::CTL, DA>(P.blocks > 0 ? P.w_res : P.w_head, lane, A);
@@ -892,11 +1073,11 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
 // (a group's latency grows with its npt_of(S) position tiles, so e.g. 3000
 // leaves run as 2 rounds of S = 6 (16 tiles), not 2 rounds of S = 8 (21 tiles)).
 __host__ __device__ inline int group_size(uint32_t count, uint32_t grid) {
-    const uint32_t cap = grid * (uint32_t)kS;
+    const uint32_t cap = grid * (uint32_t)kSRun;
     const uint32_t rounds = count ? (count + cap - 1) / cap : 1u;
     const uint32_t per = grid * rounds;
     const int g = (int)((count + per - 1) / per);
-    return g < 1 ? 1 : g > kS ? kS : g;
+    return g < 1 ? 1 : g > kSRun ? kSRun : g;
 }
 
 // Group size when `conc` search chains' forwards share the CUs (conc > 1): their
@@ -925,7 +1106,7 @@ __host__ __device__ inline int group_size_conc(uint32_t count, uint32_t grid, in
     if (conc <= 1 || count < kConcMinCount) return s0;
     float best = 3.0e38f;
     int bs = s0;
-    for (int S = s0; S <= kS; ++S) {
+    for (int S = s0; S <= kSRun; ++S) {
         const uint32_t wgs = (count + S - 1) / S, rounds = (wgs + grid - 1) / grid;
         const float cu = (float)wgs * kGroupCycles[S] + (float)(wgs < grid ? wgs : grid) * kLaunchCycles;
         const float lat = (float)rounds * kGroupCycles[S] + kLaunchCycles;
@@ -939,12 +1120,12 @@ __host__ __device__ inline int group_size_conc(uint32_t count, uint32_t grid, in
 }
 
 // The group loop of one (wave, group size) variant.
-template <int W, int S, bool FROM_X>
+template <int W, int S, bool FROM_X, int KH>
 __device__ __forceinline__ void run_groups(uint8_t *smem, const NetParams &P, uint32_t count, int ngroups,
                                            const uint64_t *__restrict__ mine, const uint64_t *__restrict__ theirs,
                                            const float *__restrict__ x, float *__restrict__ priors,
                                            float *__restrict__ value, float *__restrict__ logits, int tid) {
-    constexpr int wave = W;
+    constexpr int wave = KH == 2 ? -1 : W;   // (stamps: one wave of each SIMD pair)
     const int lane = tid & 63;
     for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
         // hide the lane id from loop-invariant code motion: the trunk geometry (and
@@ -974,7 +1155,7 @@ __device__ __forceinline__ void run_groups(uint8_t *smem, const NetParams &P, ui
             stamp(P, wave, lane, 18);
         }
 #endif
-        if (!FROM_X) {   // neighbour planes N[s][k]: k = tap*3 + plane, shifted so bit b = value at b's neighbour
+        if (!FROM_X && tid < kStemThreads) {   // neighbour planes N[s][k]: k = tap*3 + plane, shifted so bit b = value at b's neighbour
             const int s = tid >> 5, k = tid & 31;
             uint64_t v = 0;
             if (k < 27 && s < valid) {
@@ -995,7 +1176,7 @@ __device__ __forceinline__ void run_groups(uint8_t *smem, const NetParams &P, ui
         __syncthreads();
         stamp(P, wave, lane, 0);
         if (grp == (int)blockIdx.x) stamp_real(P, wave, lane, 22);
-        torso_and_heads<W, S, FROM_X>(smem, P, x, base, valid, ln, g, aux);
+        torso_and_heads<W, S, FROM_X, KH>(smem, P, x, base, valid, ln, g, aux);
         __syncthreads();
         stamp(P, wave, lane, 15);
         if (tid < valid) {
@@ -1050,11 +1231,24 @@ __device__ __forceinline__ void dispatch_wave(uint8_t *smem, const NetParams &P,
                                               const uint64_t *__restrict__ mine, const uint64_t *__restrict__ theirs,
                                               const float *__restrict__ x, float *__restrict__ priors,
                                               float *__restrict__ value, float *__restrict__ logits, int wave, int tid) {
+#ifdef SPAI_W8
+    constexpr int K0 = 1, K1 = 2;   // waves 0-3: the first K half of each tap, 4-7: the second
+#else
+    constexpr int K0 = 0, K1 = 0;
+#endif
     switch (wave) {
-    case 0: run_groups<0, S, FROM_X>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
-    case 1: run_groups<1, S, FROM_X>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
-    case 2: run_groups<2, S, FROM_X>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
-    default: run_groups<3, S, FROM_X>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
+    case 0: run_groups<0, S, FROM_X, K0>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
+    case 1: run_groups<1, S, FROM_X, K0>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
+    case 2: run_groups<2, S, FROM_X, K0>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
+    case 3: run_groups<3, S, FROM_X, K0>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
+#ifdef SPAI_W8
+    case 4: run_groups<0, S, FROM_X, K1>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
+    case 5: run_groups<1, S, FROM_X, K1>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
+    case 6: run_groups<2, S, FROM_X, K1>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
+    default: run_groups<3, S, FROM_X, K1>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
+#else
+    default: break;
+#endif
     }
 }
 
@@ -1075,21 +1269,22 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
     // launch constants (stem weights, every conv bias): their loads are issued
     // together, beside the leaf count's, and land in LDS before the group loop
     // (staged inside it they were two more dependent round trips per launch)
-    const uint4 ws = P.w_stem[tid];   // 256 x 16 B
-    const int nbias = (2 * P.blocks + 2) * kHid;
+    const bool setup = kThreads == kStemThreads || tid < kStemThreads;
+    const uint4 ws = setup ? P.w_stem[tid] : make_uint4(0u, 0u, 0u, 0u);   // 256 x 16 B
+    const int nbias = setup ? (2 * P.blocks + 2) * kHid : 0;
     float bv[kBiasPer];
 #pragma unroll
-    for (int j = 0; j < kBiasPer; ++j) bv[j] = tid + j * kThreads < nbias ? P.b_conv[tid + j * kThreads] : 0.f;
+    for (int j = 0; j < kBiasPer; ++j) bv[j] = tid + j * kStemThreads < nbias ? P.b_conv[tid + j * kStemThreads] : 0.f;
     const uint32_t count = count_ptr ? *count_ptr : count_imm;
-    const int S = force_s > 0 ? force_s : group_size_conc(count, gridDim.x, conc);
+    const int S = force_s > 0 ? min(force_s, kSRun) : group_size_conc(count, gridDim.x, conc);
     const int ngroups = (int)((count + S - 1) / S);
     if ((int)blockIdx.x >= ngroups) return;
     if (tid < 64) ((uint32_t *)(smem + kZ))[tid] = 0u;   // the zero blocks below X and Y
     else if (tid < 128) ((uint32_t *)(smem + kZ1))[tid - 64] = 0u;
-    ((uint4 *)(smem + kWStem))[tid] = ws;
+    if (setup) ((uint4 *)(smem + kWStem))[tid] = ws;
 #pragma unroll
     for (int j = 0; j < kBiasPer; ++j)
-        if (tid + j * kThreads < nbias) ((float *)(smem + kBias))[tid + j * kThreads] = bv[j];
+        if (tid + j * kStemThreads < nbias) ((float *)(smem + kBias))[tid + j * kStemThreads] = bv[j];
 #ifdef SPAI_DIAG_ENTRY
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     stamp(P, tid >> 6, tid & 63, 17);
@@ -1100,7 +1295,7 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
     if constexpr (FROM_X) {
-        dispatch_wave<kS, true>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid);
+        dispatch_wave<kSRun, true>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid);
     } else {
 #ifdef SPAI_ONLY_S
         dispatch_wave<SPAI_ONLY_S, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid);
@@ -1110,10 +1305,14 @@ __global__ __launch_bounds__(kThreads) void k_forward(const uint32_t *__restrict
         case 2: dispatch_wave<2, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid); break;
         case 3: dispatch_wave<3, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid); break;
         case 4: dispatch_wave<4, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid); break;
+#ifdef SPAI_W8
+        default: dispatch_wave<5, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid); break;
+#else
         case 5: dispatch_wave<5, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid); break;
         case 6: dispatch_wave<6, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid); break;
         case 7: dispatch_wave<7, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid); break;
         default: dispatch_wave<8, false>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, wave, tid); break;
+#endif
         }
 #endif
     }
@@ -1432,7 +1631,7 @@ int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
     std::vector<uint64_t> m, t;
     random_positions(cnt, m, t);
     const char *es = std::getenv("SPAI_PHASE_S");   // diagnostic: group size to time (default 8)
-    const int S = es ? std::max(1, std::min(kS, std::atoi(es))) : kS;
+    const int S = es ? std::max(1, std::min(kSRun, std::atoi(es))) : kSRun;
     uint32_t grid = (cnt + S - 1) / S;
     if (const char *eg = std::getenv("SPAI_PHASE_GRID"))   // fewer workgroups: the stamps keep each one's LAST group
         grid = std::min<uint32_t>(grid, (uint32_t)std::max(1, std::atoi(eg)));
@@ -1506,7 +1705,7 @@ int net_forward_x(spai_net *n, uint32_t cnt, const float *x, float *logits, floa
     if (n->dtype == SPAI_DTYPE_F32) {
         SPAI_TRY(net_f32_launch(n, st, nullptr, cnt, nullptr, nullptr, n->io_x.p, nullptr, n->io_value.p, n->io_logits.p));
     } else {
-        k_forward<true><<<(cnt + kS - 1) / kS, kThreads, 0, st>>>(nullptr, cnt, kS, 1, nullptr, nullptr, n->io_x.p,
+        k_forward<true><<<(cnt + kSRun - 1) / kSRun, kThreads, 0, st>>>(nullptr, cnt, kSRun, 1, nullptr, nullptr, n->io_x.p,
                                                                  params_of(n), nullptr, n->io_value.p, n->io_logits.p);
         SPAI_HIP(hipGetLastError());
     }

@@ -710,3 +710,30 @@ def test_learner_model_train_epochs(spai, oracle):
     check_learner_params(P, ref, all_grads, blocks, 64, len(all_grads), tol=2e-4)
     L.close()
     e.close()
+
+
+def test_self_play_sampling_frequencies(spai):
+    """learner_concurrent.rs:189-193 draws each move from WeightedIndex over
+    (visit_count as f32).powf(T) with the unseeded thread_rng, so against the
+    reference the move draw can only match in distribution.  Over >= 10^5 draws
+    of the device move step (k_advance: Philox uniform, WeightedIndex over the
+    visits^T table; 6400 games, hash evaluator), the played child's rank among
+    its position's children (by visits) must fit P(child) = N^T / sum N^T at
+    T = 1.25 (chi-square, tests/sampling_stats.py), and the same draws must
+    reject plain visit counts (T = 1) and T = 1.5 -- the exponent is applied.
+    (The bit-exact streams of test_self_play_device_sampling_matches_oracle pin
+    the arithmetic itself.)"""
+    from sampling_stats import rank_chi2
+    n_games, sims, T = 6400, 32, 1.25
+    e = spai.Engine(num_searches=sims, max_trees=n_games, eval_kind=spai.EVAL_HASH, seed=17, temperature=T)
+    games, _ = e.self_play(n_games)
+    e.close()
+    pol = np.concatenate([g["policy"] for g in games])
+    mv = np.concatenate([g["moves"] for g in games])
+    assert len(mv) >= 100_000, len(mv)
+    assert (pol[np.arange(len(mv)), mv] > 0).all()   # the played column was visited
+    c, p, obs, exp = rank_chi2(pol, mv, T)
+    assert p > 1e-4, (c, p, obs, exp)
+    for t_alt in (1.0, 1.5):
+        c_alt, p_alt, _, _ = rank_chi2(pol, mv, t_alt)
+        assert p_alt < 1e-12, (t_alt, c_alt, p_alt)
