@@ -36,9 +36,10 @@ Adds to the JSON line:
                 first 2 moves (sims/s, k_chess_forward fraction of peak)
   cpu_baseline  the CPU restatement (oracle/refcpu.py: reference data layout,
                 AoS arena with State clones, sequential tree loop) with the net
-                on libtorch CPU fp32, run in a subprocess: a small batch of games
-                played to completion in this run, beside the committed 256-game
-                record (flagged with whether it was taken on this host)
+                on libtorch CPU fp32, run in a subprocess: the reference worker's
+                batch of 100 games played to completion in this run (vs_baseline
+                divides by it), beside the committed 256-game record (flagged
+                with whether it was taken on this host)
 """
 import argparse
 import json
@@ -79,9 +80,10 @@ def parse():
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-games", type=int, default=16,
-                    help="games the CPU baseline plays to completion inside this run (~45 s on the GPU box's host)")
-    ap.add_argument("--cpu-timeout", type=float, default=240.0)
+    ap.add_argument("--cpu-games", type=int, default=100,
+                    help="games the CPU baseline plays to completion inside this run: the reference worker's batch "
+                         "(learner_concurrent.rs:50-59, num_batched_self_play_games = 100), ~2 min on the GPU box's host")
+    ap.add_argument("--cpu-timeout", type=float, default=480.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-rules-bench", action="store_true", help="skip the batched rules-kernel timing (HBM GB/s)")
     ap.add_argument("--no-chess", action="store_true", help="skip the chess window (config 4, 2 moves)")
@@ -114,9 +116,10 @@ def cpu_baseline(args):
     tree loop (reference algorithm and data layout) + libtorch CPU fp32 forward
     (oracle/refcpu.py).  Whole games, so the rate covers every game phase (an
     early-game window flatters the CPU: its early positions are its best case).
-    The committed larger run (profiles/r02/cpu_baseline.json, 256 games) is
-    reported beside it, flagged by whether it was taken on this host.  Prints one
-    JSON line."""
+    The default is the reference worker's batch, 100 games
+    (learner_concurrent.rs:50-59).  The committed larger run
+    (profiles/r02/cpu_baseline.json, 256 games) is reported beside it, flagged by
+    whether it was taken on this host.  Prints one JSON line."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import refcpu
 
@@ -448,20 +451,14 @@ def main():
         result["cpu_baseline"] = cb
         # BASELINE.md publishes no number for this metric: the ratio is against the CPU
         # reference path on whole games (same unit, sims/s over games played to
-        # completion).  The denominator is the better of the live run and the committed
-        # 256-game record, the record only when it was taken on this host (same CPU
-        # model and quota): larger CPU batches amortise libtorch's per-call cost.
+        # completion), measured in this run at the reference worker's batch of 100
+        # games; the committed 256-game record is reported beside it, not used
         if cb.get("value"):
-            rec = cb.get("record") or {}
-            use_rec = bool(rec.get("same_host")) and rec.get("sims_per_sec", 0) > cb["value"]
-            base_sims = rec["sims_per_sec"] if use_rec else cb["value"]
-            base_games = rec["games_per_sec"] if use_rec else cb["games_per_sec"]
-            result["vs_baseline"] = result["value"] / base_sims
-            result["vs_cpu_games_per_sec"] = result["games_per_sec"] / base_games
+            result["vs_baseline"] = result["value"] / cb["value"]
+            result["vs_cpu_games_per_sec"] = result["games_per_sec"] / cb["games_per_sec"]
             result["vs_baseline_basis"] = (
-                "whole-game sims/s over the CPU reference path's whole-game sims/s (%s, %.0f sims/s, %.3f games/s)"
-                % ("committed 256-game record, same host" if use_rec else "measured in this run", base_sims,
-                   base_games))
+                "whole-game sims/s over the CPU reference path's whole-game sims/s measured in this run "
+                "(%d games, %.0f sims/s, %.3f games/s)" % (args.cpu_games, cb["value"], cb["games_per_sec"]))
     if dist.rank == 0:
         print(json.dumps(result), flush=True)
     dist.close()

@@ -61,6 +61,10 @@ struct Trainer {
     engine: *mut sys::spai_engine,
     learner: *mut sys::spai_learner,
     n_params: usize,
+    // VarStore fingerprint after the learner's last write-back: a different one
+    // means the trainer's variables were changed from outside (VarStore::load /
+    // copy), and the learner is rebuilt from them rather than overwriting them
+    fingerprint: (f64, f64),
 }
 unsafe impl Send for Trainer {}
 
@@ -171,6 +175,9 @@ impl Net {
         let n = z.len();
         assert!(x.len() == n * 126 && pi.len() == n * 7, "train batch shapes: [n][3][6][7], [n][7], [n](x1)");
         let mut g = self.trainer.lock().unwrap();
+        if g.as_ref().map_or(false, |t| t.fingerprint != self.fingerprint()) {
+            *g = None;   // Drop destroys the stale learner and its engine
+        }
         if g.is_none() {
             let mut cfg = sys::spai_config::default();
             sys::check(unsafe { sys::spai_config_default(sys::SPAI_GAME_CONNECT4, &mut cfg) });
@@ -185,7 +192,7 @@ impl Net {
             sys::check(unsafe {
                 sys::spai_learner_create(e, self.blocks as i32, 64, p.as_ptr(), p.len(), std::ptr::null(), &mut l)
             });
-            *g = Some(Trainer { engine: e, learner: l, n_params: p.len() });
+            *g = Some(Trainer { engine: e, learner: l, n_params: p.len(), fingerprint: (f64::NAN, f64::NAN) });
         }
         let t = g.as_mut().unwrap();
         let mut loss = [0f32; 3];
@@ -203,6 +210,7 @@ impl Net {
             off += k;
         }
         assert_eq!(off, p.len(), "VarStore variables vs the device learner's flat parameters");
+        t.fingerprint = self.fingerprint();
         loss[0] as f64
     }
 }

@@ -277,8 +277,17 @@ __device__ __forceinline__ void residual_mfma(const uint8_t *smem, int out, int 
 template <int P>
 __device__ __forceinline__ void forward_body(uint8_t *smem, uint32_t count, uint32_t slot0,
                                              const uint16_t *__restrict__ x, const NetW &W, float *__restrict__ logits,
-                                             float *__restrict__ value, int tid, int lane, int wave) {
+                                             float *__restrict__ value, int tid_in, int lane_in, int wave) {
     constexpr int NT = 4 * P, ROWS = 64 * P, TPW = NT / kWaves;
+    // hide the thread id from loop-invariant code motion: the per-lane addresses of
+    // every layer hoisted out of the pass loop stayed live across it and were
+    // spilled to scratch (~100 8-byte slots stored per wave and launch, reloaded
+    // every pass); recomputed per pass they cost a few VALU
+    int tid = tid_in;
+    asm volatile("" : "+v"(tid));
+    tid &= kThreads - 1;
+    const int lane = tid & 63;
+    (void)lane_in;
     // stage the input planes (bf16 [cell][32]) into buffer B, chunks 0..3 of each row; zero row
     for (int i = tid; i < ROWS * 4; i += kThreads) {
         const int v = i >> 2, c = i & 3;

@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <vector>
@@ -153,17 +154,118 @@ __global__ void k_pack_all(const float *__restrict__ P, const uint32_t *__restri
     wall[d[6] + i] = v;
 }
 
+// BatchNorm (train mode) of a conv's input, applied while the consumer conv
+// stages it (MODE & kBnIn): the producer conv left per-(channel, sample)
+// partials {sum, centred sum of squares} over the 42 cells (MODE & kStatsOut);
+// every consumer workgroup merges the B partials of each input channel in the
+// same fixed order (Chan's pairwise variance: N var = sum_b Q_b + 42 sum_b
+// (m_b - mean)^2), so all of them hold the same mean / invstd, and stages
+// a = relu(gamma (z - mean) invstd + beta [+ res]).  The slice-0 workgroups of
+// each sample write a (the backward's mask and weight-gradient input), the first
+// workgroup the batch statistics and the running statistics (momentum, unbiased
+// variance) -- what k_bn_fwd did in a kernel of its own.
+constexpr int kBnIn = 1, kStatsOut = 2;
+struct BnIn {
+    const float2 *part;           // [cin][B] producer partials
+    const float *gamma, *beta;
+    const float *res;             // residual (block input) [B][cin][42], or null
+    float *a_out;                 // activations [B][cin][42]
+    float *mean, *invstd, *run_mean, *run_var;
+    int B;
+    float eps, momentum;
+};
+constexpr int kBnStatFloats = 4 * 64;   // LDS: mean, invstd, gamma, beta per input channel
+
+// per-channel statistics of the input from the producer's partials -> LDS st[4][64]
+__device__ __forceinline__ void bn_in_stats(const BnIn &bn, int cin, float *st) {
+    const int c = threadIdx.x >> 2, qq = threadIdx.x & 3, B = bn.B;
+    const float2 *pp = bn.part + (size_t)c * B;
+    float s = 0.f;
+    if (c < cin)
+        for (int b = qq; b < B; b += 4) s += pp[b].x;
+    s += __shfl_xor(s, 1, 64);   // the 4 quarters in a fixed order, the same value on all 4 lanes
+    s += __shfl_xor(s, 2, 64);
+    const int n = B * kCells;
+    const float mu = s / (float)n;
+    float q = 0.f;
+    if (c < cin)
+        for (int b = qq; b < B; b += 4) {
+            const float2 v = pp[b];
+            const float d = v.x / (float)kCells - mu;
+            q += v.y + (float)kCells * (d * d);
+        }
+    q += __shfl_xor(q, 1, 64);
+    q += __shfl_xor(q, 2, 64);
+    const float var = q / (float)n;
+    const float is = 1.0f / sqrtf(var + bn.eps);
+    if (qq == 0 && c < cin) {
+        st[c] = mu;
+        st[64 + c] = is;
+        st[128 + c] = bn.gamma[c];
+        st[192 + c] = bn.beta[c];
+        if (blockIdx.x == 0 && blockIdx.y == 0) {
+            bn.mean[c] = mu;
+            bn.invstd[c] = is;
+            bn.run_mean[c] = (1.0f - bn.momentum) * bn.run_mean[c] + bn.momentum * mu;
+            bn.run_var[c] = (1.0f - bn.momentum) * bn.run_var[c] +
+                            bn.momentum * (n > 1 ? var * (float)n / (float)(n - 1) : var);
+        }
+    }
+}
+
+// stage_planes_fast of relu(bn(z) [+ res]) (k_bn_fwd's arithmetic); a written by the slice-0 workgroups
+template <int CINP>
+__device__ __forceinline__ void stage_planes_bn(const float *__restrict__ zb, int cin, const BnIn &bn, size_t boff,
+                                                const float *st, float *xs) {
+    const int t = threadIdx.x;
+    if (t < 252) {
+        const int c0 = t / kCells, cell = t - c0 * kCells;
+        float *dst = xs + c0 * kPlane + (cell / kCols + 1) * 9 + cell % kCols + 1;
+        float v[(CINP + 5) / 6], r[(CINP + 5) / 6];
+#pragma unroll
+        for (int j = 0; j < (CINP + 5) / 6; ++j) {
+            v[j] = c0 + 6 * j < cin ? zb[t + 252 * j] : 0.f;
+            r[j] = bn.res && c0 + 6 * j < cin ? bn.res[boff + t + 252 * j] : 0.f;
+        }
+        const bool wa = bn.a_out && blockIdx.y == 0;
+#pragma unroll
+        for (int j = 0; j < (CINP + 5) / 6; ++j) {
+            const int c = c0 + 6 * j;
+            if (c < CINP) {
+                float a = 0.f;
+                if (c < cin) {
+                    float y = st[128 + c] * ((v[j] - st[c]) * st[64 + c]) + st[192 + c];
+                    if (bn.res) y += r[j];
+                    a = fmaxf(y, 0.f);
+                    if (wa) bn.a_out[boff + t + 252 * j] = a;
+                }
+                dst[6 * kPlane * j] = a;
+            }
+        }
+    }
+    if (t < 240) {
+        const int c0 = t / 30, bi = t - c0 * 30;
+        const int k = bi - 18;
+        const int off = bi < 9 ? bi : bi < 18 ? 63 + bi - 9 : 9 * (1 + k / 2) + ((k & 1) ? 8 : 0);
+        float *dst = xs + c0 * kPlane + off;
+#pragma unroll
+        for (int j = 0; j < (CINP + 7) / 8; ++j)
+            if (c0 + 8 * j < CINP) dst[8 * kPlane * j] = 0.f;
+    }
+}
+
 // workgroup (sample, slice): 3 position tiles (48 rows, 42 real) x NT channel
 // tiles of output channels [16 NT slice, 16 NT (slice + 1)); wave w owns channel
 // tile w % NT and K part w / NT (KS = 4/NT parts, summed in LDS in a fixed
 // order).  CINP (input channels padded to 4) and NT are compile-time, so the
 // k-loop unrolls fully and the weight loads of a whole part are in flight
 // together.  coutp_all = the packed matrix's row length (all output channels).
-template <int CINP, int NT, int MTS = 3>
+template <int CINP, int NT, int MODE = 0, int MTS = 3>
 __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict__ in, int cin,
                                                         const float *__restrict__ wk, const float *__restrict__ bias,
                                                         int cout, int coutp_all, float *__restrict__ out,
-                                                        int accumulate) {
+                                                        int accumulate, BnIn bn, float2 *__restrict__ stats_out,
+                                                        int stats_b) {
     constexpr int KS = 4 / NT, CSN = CINP / 4, KSTEPS = 9 * CSN, PER = KSTEPS / KS;
     static_assert(4 % NT == 0 && KSTEPS % KS == 0, "4 waves: NT channel tiles x KS whole K parts");
     extern __shared__ float sm[];
@@ -179,7 +281,14 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
     float bq[PER];
 #pragma unroll
     for (int i = 0; i < PER; ++i) bq[i] = wl[(size_t)i * 4 * coutp_all];
-    stage_planes_fast<CINP>(in + (size_t)b * cin * kCells, cin, xs);
+    if constexpr ((MODE & kBnIn) != 0) {
+        float *st = sm + CINP * kPlane + 2 * 2304;
+        bn_in_stats(bn, cin, st);
+        __syncthreads();
+        stage_planes_bn<CINP>(in + (size_t)b * cin * kCells, cin, bn, (size_t)b * cin * kCells, st, xs);
+    } else {
+        stage_planes_fast<CINP>(in + (size_t)b * cin * kCells, cin, xs);
+    }
     __syncthreads();
     // MTS = 3: the workgroup covers all 3 position tiles and blockIdx.y picks the
     // channel slice; MTS = 1: blockIdx.y picks the position tile (all channels)
@@ -243,7 +352,7 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
     }
     const int n = co0 + nt * 16 + row;   // D[row = 4 kq + r][col = lane & 15]: col = channel, row = position
     if (n >= cout) return;
-    const float bn = bias ? bias[n] : 0.f;
+    const float bv = bias ? bias[n] : 0.f;
     float *ob = out + ((size_t)b * cout + n) * kCells;
 #pragma unroll
     for (int mt = 0; mt < MTS; ++mt)
@@ -251,10 +360,34 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
         for (int r = 0; r < 4; ++r) {
             const int p = (mt0 + mt) * 16 + 4 * kq + r;
             if (p < kCells) {
-                const float v = acc[mt][r] + bn;
+                const float v = acc[mt][r] + bv;
                 ob[p] = accumulate ? ob[p] + v : v;
             }
         }
+    if constexpr ((MODE & kStatsOut) != 0) {   // the consumer's BN partials of channel n, sample b
+        static_assert(MTS == 3, "statistics need the whole board");
+        float s = 0.f;
+#pragma unroll
+        for (int mt = 0; mt < MTS; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if ((mt0 + mt) * 16 + 4 * kq + r < kCells) s += acc[mt][r] + bv;
+        s += __shfl_xor(s, 16, 64);   // the 4 lanes of the channel, a fixed order, the same value on each
+        s += __shfl_xor(s, 32, 64);
+        const float m = s / (float)kCells;
+        float q = 0.f;
+#pragma unroll
+        for (int mt = 0; mt < MTS; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if ((mt0 + mt) * 16 + 4 * kq + r < kCells) {
+                    const float d = (acc[mt][r] + bv) - m;
+                    q += d * d;
+                }
+        q += __shfl_xor(q, 16, 64);
+        q += __shfl_xor(q, 32, 64);
+        if (kq == 0) stats_out[(size_t)n * stats_b + b] = make_float2(s, q);
+    }
 }
 
 // weight-gradient partials: workgroup (chunk, group) accumulates, over the
@@ -704,6 +837,7 @@ int learner_alloc_batch(spai_learner *L, uint32_t B) {
     }
     SPAI_TRY(L->d0.alloc(act));
     SPAI_TRY(L->d1.alloc(act));
+    SPAI_TRY(L->bn_part.alloc((size_t)(2 * L->blocks + 1) * L->hidden * B * 2));
     SPAI_TRY(L->dlogits.alloc((size_t)B * 7));
     SPAI_TRY(L->dpre.alloc(B));
     SPAI_TRY(L->loss_terms.alloc((size_t)B * 2));
@@ -721,41 +855,52 @@ int learner_alloc_batch(spai_learner *L, uint32_t B) {
 // its own workgroup with the K split over its 4 waves (grid B x coutp/16: 4x
 // the workgroups of one per sample); the stem's input (4 padded channels, 9
 // k-steps) keeps one workgroup per sample with a wave per channel tile.
-template <int CINP>
+template <int CINP, int MODE>
 int launch_conv_t(int B, size_t lds, hipStream_t st, const float *in, int cin, const float *wk, const float *bias,
-                  int cout, float *out, int acc) {
+                  int cout, float *out, int acc, const BnIn &bn, float2 *stats) {
     constexpr int ks = 9 * CINP / 4;
     const int nt = round16(cout) / 16;
 #ifdef SPAI_SLICE_NT2   // variant: 32-channel slices, the K split over 2 wave pairs
     if constexpr (ks % 2 == 0) {
         if (nt % 2 == 0) {
-            k_conv_mfma<CINP, 2><<<dim3(B, nt / 2), kThreads, lds, st>>>(in, cin, wk, bias, cout, 16 * nt, out, acc);
+            k_conv_mfma<CINP, 2, MODE><<<dim3(B, nt / 2), kThreads, lds, st>>>(in, cin, wk, bias, cout, 16 * nt, out,
+                                                                              acc, bn, stats, B);
             return SPAI_OK;
         }
     }
 #endif
     if constexpr (ks % 4 == 0) {
-        k_conv_mfma<CINP, 1><<<dim3(B, nt), kThreads, lds, st>>>(in, cin, wk, bias, cout, 16 * nt, out, acc);
+        k_conv_mfma<CINP, 1, MODE><<<dim3(B, nt), kThreads, lds, st>>>(in, cin, wk, bias, cout, 16 * nt, out, acc, bn,
+                                                                      stats, B);
         return SPAI_OK;
     }
     if (nt == 4) {
-        k_conv_mfma<CINP, 4><<<dim3(B), kThreads, lds, st>>>(in, cin, wk, bias, cout, 64, out, acc);
+        k_conv_mfma<CINP, 4, MODE><<<dim3(B), kThreads, lds, st>>>(in, cin, wk, bias, cout, 64, out, acc, bn, stats, B);
         return SPAI_OK;
     }
     set_error("learner conv: %d input / %d output channels not built", cin, cout);
     return SPAI_ERR_UNSUPPORTED;
 }
 
+// bn: the input's BatchNorm applied while staging (in = the producer's z), or
+// null; stats: this conv's per-(channel, sample) BN partials for its consumer, or null
 int launch_conv(const float *in, int cin, const float *wk, const float *bias, int cout, float *out, int B, bool acc,
-                hipStream_t st) {
+                hipStream_t st, const BnIn *bn = nullptr, float2 *stats = nullptr) {
     const int cinp = round4(cin);
-    const size_t lds = ((size_t)cinp * kPlane + 2 * 2304) * sizeof(float);
+    const size_t lds = ((size_t)cinp * kPlane + 2 * 2304 + (bn ? kBnStatFloats : 0)) * sizeof(float);
     const int a = acc ? 1 : 0;
-    switch (cinp) {
-    case 4: return launch_conv_t<4>(B, lds, st, in, cin, wk, bias, cout, out, a);
-    case 32: return launch_conv_t<32>(B, lds, st, in, cin, wk, bias, cout, out, a);
-    case 64: return launch_conv_t<64>(B, lds, st, in, cin, wk, bias, cout, out, a);
-    default: set_error("learner conv: %d input channels not built", cin); return SPAI_ERR_UNSUPPORTED;
+    const BnIn none{};
+    const BnIn &b = bn ? *bn : none;
+    const int mode = (bn ? kBnIn : 0) | (stats ? kStatsOut : 0);
+    switch (cinp * 4 + mode) {
+    case 4 * 4 + 0: return launch_conv_t<4, 0>(B, lds, st, in, cin, wk, bias, cout, out, a, b, stats);
+    case 4 * 4 + kStatsOut: return launch_conv_t<4, kStatsOut>(B, lds, st, in, cin, wk, bias, cout, out, a, b, stats);
+    case 32 * 4 + 0: return launch_conv_t<32, 0>(B, lds, st, in, cin, wk, bias, cout, out, a, b, stats);
+    case 64 * 4 + 0: return launch_conv_t<64, 0>(B, lds, st, in, cin, wk, bias, cout, out, a, b, stats);
+    case 64 * 4 + kBnIn: return launch_conv_t<64, kBnIn>(B, lds, st, in, cin, wk, bias, cout, out, a, b, stats);
+    case 64 * 4 + (kBnIn | kStatsOut):
+        return launch_conv_t<64, kBnIn | kStatsOut>(B, lds, st, in, cin, wk, bias, cout, out, a, b, stats);
+    default: set_error("learner conv: %d input channels (mode %d) not built", cin, mode); return SPAI_ERR_UNSUPPORTED;
     }
 }
 
@@ -910,7 +1055,7 @@ void learner_destroy(spai_learner *L) {
     L->pack_desc.release();
     if (L->stage) (void)hipHostFree(L->stage);
     if (L->host_buf) (void)hipHostFree(L->host_buf);
-    for (auto *b : {&L->p, &L->g, &L->bsum, &L->m, &L->v, &L->wt, &L->batch_in, &L->d0, &L->d1, &L->dlogits,
+    for (auto *b : {&L->p, &L->g, &L->bsum, &L->m, &L->v, &L->wt, &L->batch_in, &L->d0, &L->d1, &L->bn_part, &L->dlogits,
                     &L->dpre, &L->loss_terms, &L->run_buf})
         b->release();
     L->run_idx.release();
@@ -962,15 +1107,57 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
         k_bn_fwd<<<c.co, kBn, 0, st>>>(L->z[l].p, c.co, (int)B, eps, mom, L->mean[l].p, L->invstd[l].p, P + c.mu,
                                        P + c.var, P + c.g, P + c.be, res, L->a[l].p);
     };
-    conv_bn_act(0, x_in, nullptr);
-    const float *h = L->a[0].p;
-    for (int k = 0; k < L->blocks; ++k) {   // relu(h + BN(conv(relu(BN(conv(h)))))) (model/mod.rs:152-165)
-        conv_bn_act(1 + 2 * k, h, nullptr);
-        conv_bn_act(2 + 2 * k, L->a[1 + 2 * k].p, h);
-        h = L->a[2 + 2 * k].p;
+    // SPAI_LEARNER_BN_FUSE=0: a k_bn_fwd kernel after every conv (A/B knob); default:
+    // the trunk's BN + ReLU (+ residual) run inside the next conv's staging (BnIn)
+    static const bool fuse = [] {
+        const char *v = std::getenv("SPAI_LEARNER_BN_FUSE");
+        return !v || std::atoi(v) != 0;
+    }();
+    const float *h = nullptr;
+    if (fuse) {
+        const int last = 2 * L->blocks;   // the trunk's last conv
+        auto part_of = [&](int l) { return (float2 *)L->bn_part.p + (size_t)l * L->hidden * B; };
+        // layer l's BN input to its consumer: the residual is the block input a[l - 2] for a block's second conv
+        auto bn_of = [&](int l) {
+            const spai_learner::Conv &c = L->convs[l];
+            return BnIn{part_of(l), P + c.g, P + c.be, (l >= 2 && l % 2 == 0) ? L->a[l - 2].p : nullptr, L->a[l].p,
+                        L->mean[l].p, L->invstd[l].p, P + c.mu, P + c.var, (int)B, eps, mom};
+        };
+        {
+            const spai_learner::Conv &c = L->convs[0];
+            crc = launch_conv(x_in, c.ci, W + c.wk, P + c.b, c.co, L->z[0].p, (int)B, false, st, nullptr, part_of(0));
+        }
+        for (int l = 1; l <= last && crc == SPAI_OK; ++l) {   // relu(h + BN(conv(relu(BN(conv(h)))))), model/mod.rs:152-165
+            const spai_learner::Conv &c = L->convs[l];
+            const BnIn b = bn_of(l - 1);
+            crc = launch_conv(L->z[l - 1].p, c.ci, W + c.wk, P + c.b, c.co, L->z[l].p, (int)B, false, st, &b, part_of(l));
+        }
+        if (crc == SPAI_OK) {   // the policy head conv applies the trunk's last BN and writes the trunk output
+            const spai_learner::Conv &c = L->convs[pol];
+            const BnIn b = bn_of(last);
+            crc = launch_conv(L->z[last].p, c.ci, W + c.wk, P + c.b, c.co, L->z[pol].p, (int)B, false, st, &b, nullptr);
+        }
+        h = L->a[last].p;
+        if (crc == SPAI_OK) {
+            const spai_learner::Conv &c = L->convs[val];
+            crc = launch_conv(h, c.ci, W + c.wk, P + c.b, c.co, L->z[val].p, (int)B, false, st);
+        }
+        for (int l : {pol, val}) {
+            const spai_learner::Conv &c = L->convs[l];
+            k_bn_fwd<<<c.co, kBn, 0, st>>>(L->z[l].p, c.co, (int)B, eps, mom, L->mean[l].p, L->invstd[l].p, P + c.mu,
+                                           P + c.var, P + c.g, P + c.be, nullptr, L->a[l].p);
+        }
+    } else {
+        conv_bn_act(0, x_in, nullptr);
+        h = L->a[0].p;
+        for (int k = 0; k < L->blocks; ++k) {   // relu(h + BN(conv(relu(BN(conv(h)))))) (model/mod.rs:152-165)
+            conv_bn_act(1 + 2 * k, h, nullptr);
+            conv_bn_act(2 + 2 * k, L->a[1 + 2 * k].p, h);
+            h = L->a[2 + 2 * k].p;
+        }
+        conv_bn_act(pol, h, nullptr);
+        conv_bn_act(val, h, nullptr);
     }
-    conv_bn_act(pol, h, nullptr);
-    conv_bn_act(val, h, nullptr);
     k_heads_loss<<<B, kThreads, 0, st>>>(L->a[pol].p, L->a[val].p, P + L->pol_w, P + L->pol_b, P + L->val_w,
                                          P + L->val_b, pi_in, z_in, (int)B, L->dlogits.p, L->dpre.p,
                                          L->loss_terms.p);

@@ -1234,7 +1234,7 @@ __device__ __forceinline__ void dispatch_wave(uint8_t *smem, const NetParams &P,
 #ifdef SPAI_W8
     constexpr int K0 = 1, K1 = 2;   // waves 0-3: the first K half of each tap, 4-7: the second
 #else
-    constexpr int K0 = 0, K1 = 0;
+    constexpr int K0 = 0;
 #endif
     switch (wave) {
     case 0: run_groups<0, S, FROM_X, K0>(smem, P, count, ngroups, mine, theirs, x, priors, value, logits, tid); break;
