@@ -164,7 +164,7 @@ __global__ void k_pack_all(const float *__restrict__ P, const uint32_t *__restri
 // each sample write a (the backward's mask and weight-gradient input), the first
 // workgroup the batch statistics and the running statistics (momentum, unbiased
 // variance) -- what k_bn_fwd did in a kernel of its own.
-constexpr int kBnIn = 1, kStatsOut = 2;
+constexpr int kBnIn = 1, kStatsOut = 2, kBnGrad = 4, kGradStats = 8;
 struct BnIn {
     const float2 *part;           // [cin][B] producer partials
     const float *gamma, *beta;
@@ -174,7 +174,104 @@ struct BnIn {
     int B;
     float eps, momentum;
 };
-constexpr int kBnStatFloats = 4 * 64;   // LDS: mean, invstd, gamma, beta per input channel
+constexpr int kBnStatFloats = 5 * 64;   // LDS: per input channel 4 (forward) or 5 (backward) statistics
+
+// The backward of a = relu(bn(z) [+ res]) fused the same way (kBnGrad): the
+// producer of da (the data gradient of the layer above, kGradStats) leaves per
+// (channel, sample) partials {sum dy, sum dy xhat} with dy = da [a > 0] and
+// xhat = (z - mean) invstd; the consumer (this layer's data-gradient conv)
+// merges them into dbeta = sum dy and dgamma = sum dy xhat and stages
+// dz = gamma invstd / N (N dy - dbeta - xhat dgamma) (k_bn_bwd's arithmetic),
+// writing dz for the weight gradient and dy for the residual's skip path from
+// its slice-0 workgroups.  The conv bias gradient (sum dz) comes from the weight
+// gradient (a column of ones, k_wgrad_mfma BIAS).
+struct BnGrad {
+    const float2 *part;           // [c][B] {sum dy, sum dy xhat} of this layer
+    const float *a, *z, *mean, *invstd, *gamma;
+    float *dz_out, *dy_out;       // [B][c][42] (dy_out may be null)
+    float *dgamma, *dbeta;
+    int B;
+};
+struct GradStats {                // the partials for the layer whose da this conv produces
+    const float *a, *z, *mean, *invstd;
+    float2 *part;                 // [c][B]
+};
+
+__device__ __forceinline__ void bn_grad_stats(const BnGrad &bg, int cin, float *st) {
+    const int c = threadIdx.x >> 2, qq = threadIdx.x & 3, B = bg.B;
+    const float2 *pp = bg.part + (size_t)c * B;
+    float s1 = 0.f, s2 = 0.f;
+    if (c < cin)
+        for (int b = qq; b < B; b += 4) {
+            const float2 v = pp[b];
+            s1 += v.x;
+            s2 += v.y;
+        }
+    s1 += __shfl_xor(s1, 1, 64);
+    s1 += __shfl_xor(s1, 2, 64);
+    s2 += __shfl_xor(s2, 1, 64);
+    s2 += __shfl_xor(s2, 2, 64);
+    if (qq == 0 && c < cin) {
+        const float is = bg.invstd[c];
+        st[c] = s1;
+        st[64 + c] = s2;
+        st[128 + c] = bg.mean[c];
+        st[192 + c] = is;
+        st[256 + c] = bg.gamma[c] * is / (float)(B * kCells);
+        if (blockIdx.x == 0 && blockIdx.y == 0) {
+            bg.dbeta[c] = s1;
+            bg.dgamma[c] = s2;
+        }
+    }
+}
+
+// stage dz of this layer (k_bn_bwd's arithmetic) from da, a, z; slice 0 writes dz and dy
+template <int CINP>
+__device__ __forceinline__ void stage_planes_dz(const float *__restrict__ dab, int cin, const BnGrad &bg, size_t boff,
+                                                const float *st, float *xs) {
+    const int t = threadIdx.x;
+    if (t < 252) {
+        const int c0 = t / kCells, cell = t - c0 * kCells;
+        float *dst = xs + c0 * kPlane + (cell / kCols + 1) * 9 + cell % kCols + 1;
+        constexpr int J = (CINP + 5) / 6;
+        float vd[J], va[J], vz[J];
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const bool ok = c0 + 6 * j < cin;
+            vd[j] = ok ? dab[t + 252 * j] : 0.f;
+            va[j] = ok ? bg.a[boff + t + 252 * j] : 0.f;
+            vz[j] = ok ? bg.z[boff + t + 252 * j] : 0.f;
+        }
+        const bool w = blockIdx.y == 0;
+        const float n = (float)(bg.B * kCells);
+#pragma unroll
+        for (int j = 0; j < J; ++j) {
+            const int c = c0 + 6 * j;
+            if (c < CINP) {
+                float v = 0.f;
+                if (c < cin) {
+                    const float d = va[j] > 0.f ? vd[j] : 0.f;
+                    const float x = (vz[j] - st[128 + c]) * st[192 + c];
+                    v = st[256 + c] * (n * d - st[c] - x * st[64 + c]);
+                    if (w) {
+                        bg.dz_out[boff + t + 252 * j] = v;
+                        if (bg.dy_out) bg.dy_out[boff + t + 252 * j] = d;
+                    }
+                }
+                dst[6 * kPlane * j] = v;
+            }
+        }
+    }
+    if (t < 240) {
+        const int c0 = t / 30, bi = t - c0 * 30;
+        const int k = bi - 18;
+        const int off = bi < 9 ? bi : bi < 18 ? 63 + bi - 9 : 9 * (1 + k / 2) + ((k & 1) ? 8 : 0);
+        float *dst = xs + c0 * kPlane + off;
+#pragma unroll
+        for (int j = 0; j < (CINP + 7) / 8; ++j)
+            if (c0 + 8 * j < CINP) dst[8 * kPlane * j] = 0.f;
+    }
+}
 
 // per-channel statistics of the input from the producer's partials -> LDS st[4][64]
 __device__ __forceinline__ void bn_in_stats(const BnIn &bn, int cin, float *st) {
@@ -265,7 +362,7 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
                                                         const float *__restrict__ wk, const float *__restrict__ bias,
                                                         int cout, int coutp_all, float *__restrict__ out,
                                                         int accumulate, BnIn bn, float2 *__restrict__ stats_out,
-                                                        int stats_b) {
+                                                        int stats_b, BnGrad bg, GradStats gs) {
     constexpr int KS = 4 / NT, CSN = CINP / 4, KSTEPS = 9 * CSN, PER = KSTEPS / KS;
     static_assert(4 % NT == 0 && KSTEPS % KS == 0, "4 waves: NT channel tiles x KS whole K parts");
     extern __shared__ float sm[];
@@ -286,6 +383,11 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
         bn_in_stats(bn, cin, st);
         __syncthreads();
         stage_planes_bn<CINP>(in + (size_t)b * cin * kCells, cin, bn, (size_t)b * cin * kCells, st, xs);
+    } else if constexpr ((MODE & kBnGrad) != 0) {
+        float *st = sm + CINP * kPlane + 2 * 2304;
+        bn_grad_stats(bg, cin, st);
+        __syncthreads();
+        stage_planes_dz<CINP>(in + (size_t)b * cin * kCells, cin, bg, (size_t)b * cin * kCells, st, xs);
     } else {
         stage_planes_fast<CINP>(in + (size_t)b * cin * kCells, cin, xs);
     }
@@ -354,16 +456,41 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
     if (n >= cout) return;
     const float bv = bias ? bias[n] : 0.f;
     float *ob = out + ((size_t)b * cout + n) * kCells;
+    float fin[MTS][4];   // the stored values (kGradStats)
 #pragma unroll
     for (int mt = 0; mt < MTS; ++mt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int p = (mt0 + mt) * 16 + 4 * kq + r;
+            fin[mt][r] = 0.f;
             if (p < kCells) {
                 const float v = acc[mt][r] + bv;
-                ob[p] = accumulate ? ob[p] + v : v;
+                fin[mt][r] = accumulate ? ob[p] + v : v;
+                ob[p] = fin[mt][r];
             }
         }
+    if constexpr ((MODE & kGradStats) != 0) {   // the next BN backward's partials of channel n, sample b
+        static_assert(MTS == 3, "statistics need the whole board");
+        const size_t base = ((size_t)b * cout + n) * kCells;
+        const float mu = gs.mean[n], is = gs.invstd[n];
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int mt = 0; mt < MTS; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int p = (mt0 + mt) * 16 + 4 * kq + r;
+                if (p < kCells) {
+                    const float d = gs.a[base + p] > 0.f ? fin[mt][r] : 0.f;
+                    s1 += d;
+                    s2 += d * ((gs.z[base + p] - mu) * is);
+                }
+            }
+        s1 += __shfl_xor(s1, 16, 64);
+        s1 += __shfl_xor(s1, 32, 64);
+        s2 += __shfl_xor(s2, 16, 64);
+        s2 += __shfl_xor(s2, 32, 64);
+        if (kq == 0) gs.part[(size_t)n * stats_b + b] = make_float2(s1, s2);
+    }
     if constexpr ((MODE & kStatsOut) != 0) {   // the consumer's BN partials of channel n, sample b
         static_assert(MTS == 3, "statistics need the whole board");
         float s = 0.f;
@@ -404,15 +531,19 @@ constexpr int kWgSamples = SPAI_WG_SAMPLES;
 #define SPAI_WG_TILES 3
 #endif
 constexpr int kWgMaxTiles = SPAI_WG_TILES;   // tiles per wave (144 tiles / 12 groups / 4 waves at 64 x 64: 384 workgroups at B = 128)
-template <int CINP>
+// BIAS: one more GEMM column k = K over a plane of ones, part[..][n][K] = sum_p dz:
+// the conv bias gradient (for the layers whose BN backward runs in the data
+// gradient's staging, kBnGrad)
+template <int CINP, bool BIAS>
 __global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict__ x, int cin,
                                                          const float *__restrict__ dz, int cout, int B, int groups,
                                                          float *__restrict__ part) {
-    constexpr int K = 9 * CINP, Kp = (K + 15) & ~15, NK = Kp / 16;
+    constexpr int K = 9 * CINP, K1 = K + (BIAS ? 1 : 0), Kp = (K1 + 15) & ~15, NK = Kp / 16;
     extern __shared__ float sm[];
     const int coutp = round16(cout), NTo = coutp / 16, ntiles = NTo * NK;
     float *xs = sm;                        // [CINP][kPlane]
     float *ds = sm + CINP * kPlane;        // [coutp][44], zero past 42 and past cout
+    float *ones = ds + coutp * 44;         // BIAS: [kPlane] of 1.0
     const int chunk = blockIdx.x, group = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int row = lane & 15, kq = lane >> 4;
     // this wave's tiles: group's range [t0, t1), wave-strided
@@ -440,6 +571,8 @@ __global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict
     constexpr int ND = (64 * kCells + kThreads - 1) / kThreads;     // cout <= 64
     const int nx = cin * kCells, nd = cout * kCells;
     for (int i = threadIdx.x; i < CINP * kPlane + coutp * 44; i += kThreads) sm[i] = 0.f;
+    if (BIAS)
+        for (int i = threadIdx.x; i < kPlane; i += kThreads) ones[i] = 1.f;
     int dx[NX], dd[ND];
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
@@ -477,8 +610,8 @@ __global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict
             const int k = kt * 16 + row;                      // B[kk = position][n = k]
             const bool kval = k < K;
             const int tap = k / CINP, c = k % CINP;           // CINP: compile-time
-            // a padding column (k >= K) reads position data too: its D column is never stored
-            const float *xcol = xs + (kval ? c * kPlane + tap_off(tap) : 0);
+            // a padding column (k >= K1) reads position data too: its D column is never stored
+            const float *xcol = BIAS && k == K ? ones : xs + (kval ? c * kPlane + tap_off(tap) : 0);
 #pragma unroll
             for (int s = 0; s < 11; ++s) {
                 const float av = arow[4 * s + kq];
@@ -497,7 +630,7 @@ __global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int n = mt * 16 + 4 * kq + r;
-            if (n < cout && k < K) part[((size_t)chunk * cout + n) * K + k] = acc[j][r];
+            if (n < cout && k < K1) part[((size_t)chunk * cout + n) * K1 + k] = acc[j][r];
         }
     }
 }
@@ -512,12 +645,13 @@ __global__ __launch_bounds__(kThreads) void k_wgrad_mfma(const float *__restrict
 #define SPAI_WG_REDUCE_THREADS 64
 #endif
 constexpr int kWgReduceBatch = SPAI_WG_REDUCE_BATCH, kWgReduceThreads = SPAI_WG_REDUCE_THREADS;
-__global__ void k_wgrad_reduce(const float *__restrict__ part, int B, int cin, int cout, float *__restrict__ dw) {
+__global__ void k_wgrad_reduce(const float *__restrict__ part, int B, int cin, int cout, float *__restrict__ dw,
+                               float *__restrict__ dbias) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const int cinp = round4(cin), K = 9 * cinp;
+    const int cinp = round4(cin), K0 = 9 * cinp, K = K0 + (dbias ? 1 : 0);   // (the bias column k = K0)
     if (i < cout * K) {   // i = n * K + k: consecutive threads read consecutive partials (coalesced)
         const int n = i / K, k = i - n * K, tap = k / cinp, c = k - tap * cinp;
-        if (c < cin) {
+        if (c < cin || k == K0) {
             const float *src = part + i;
             const size_t stride = (size_t)cout * K;
             float s = 0.f;
@@ -529,7 +663,8 @@ __global__ void k_wgrad_reduce(const float *__restrict__ part, int B, int cin, i
                 for (int j = 0; j < kWgReduceBatch; ++j)
                     if (b0 + j < B) s += v[j];
             }
-            dw[((size_t)n * cin + c) * 9 + tap] = s;
+            if (k == K0) dbias[n] = s;
+            else dw[((size_t)n * cin + c) * 9 + tap] = s;
         }
     }
 }
@@ -838,12 +973,14 @@ int learner_alloc_batch(spai_learner *L, uint32_t B) {
     SPAI_TRY(L->d0.alloc(act));
     SPAI_TRY(L->d1.alloc(act));
     SPAI_TRY(L->bn_part.alloc((size_t)(2 * L->blocks + 1) * L->hidden * B * 2));
+    SPAI_TRY(L->d2.alloc(act));
+    if (L->blocks > 0) SPAI_TRY(L->dzb.alloc((size_t)2 * L->blocks * B * L->hidden * kCells));
     SPAI_TRY(L->dlogits.alloc((size_t)B * 7));
     SPAI_TRY(L->dpre.alloc(B));
     SPAI_TRY(L->loss_terms.alloc((size_t)B * 2));
     const size_t cmax = (size_t)std::max(L->hidden, 32);
     for (auto &w : L->wpart_side)   // weight-gradient partials per chunk (one buffer per side stream)
-        SPAI_TRY(w.alloc((size_t)((B + kWgSamples - 1) / kWgSamples) * cmax * 9 * round4(L->hidden)));
+        SPAI_TRY(w.alloc((size_t)((B + kWgSamples - 1) / kWgSamples) * cmax * (9 * round4(L->hidden) + 1)));
     L->max_batch = B;
     return SPAI_OK;
 }
@@ -857,25 +994,26 @@ int learner_alloc_batch(spai_learner *L, uint32_t B) {
 // k-steps) keeps one workgroup per sample with a wave per channel tile.
 template <int CINP, int MODE>
 int launch_conv_t(int B, size_t lds, hipStream_t st, const float *in, int cin, const float *wk, const float *bias,
-                  int cout, float *out, int acc, const BnIn &bn, float2 *stats) {
+                  int cout, float *out, int acc, const BnIn &bn, float2 *stats, const BnGrad &bg, const GradStats &gs) {
     constexpr int ks = 9 * CINP / 4;
     const int nt = round16(cout) / 16;
 #ifdef SPAI_SLICE_NT2   // variant: 32-channel slices, the K split over 2 wave pairs
     if constexpr (ks % 2 == 0) {
         if (nt % 2 == 0) {
             k_conv_mfma<CINP, 2, MODE><<<dim3(B, nt / 2), kThreads, lds, st>>>(in, cin, wk, bias, cout, 16 * nt, out,
-                                                                              acc, bn, stats, B);
+                                                                              acc, bn, stats, B, bg, gs);
             return SPAI_OK;
         }
     }
 #endif
     if constexpr (ks % 4 == 0) {
         k_conv_mfma<CINP, 1, MODE><<<dim3(B, nt), kThreads, lds, st>>>(in, cin, wk, bias, cout, 16 * nt, out, acc, bn,
-                                                                      stats, B);
+                                                                      stats, B, bg, gs);
         return SPAI_OK;
     }
     if (nt == 4) {
-        k_conv_mfma<CINP, 4, MODE><<<dim3(B), kThreads, lds, st>>>(in, cin, wk, bias, cout, 64, out, acc, bn, stats, B);
+        k_conv_mfma<CINP, 4, MODE><<<dim3(B), kThreads, lds, st>>>(in, cin, wk, bias, cout, 64, out, acc, bn, stats, B,
+                                                                  bg, gs);
         return SPAI_OK;
     }
     set_error("learner conv: %d input / %d output channels not built", cin, cout);
@@ -883,41 +1021,56 @@ int launch_conv_t(int B, size_t lds, hipStream_t st, const float *in, int cin, c
 }
 
 // bn: the input's BatchNorm applied while staging (in = the producer's z), or
-// null; stats: this conv's per-(channel, sample) BN partials for its consumer, or null
+// null; stats: this conv's per-(channel, sample) BN partials for its consumer, or
+// null; bg: the input (= da) turned into this layer's dz while staging (the BN
+// backward), or null; gs: the BN-backward partials of the layer whose da this
+// conv writes, or null
 int launch_conv(const float *in, int cin, const float *wk, const float *bias, int cout, float *out, int B, bool acc,
-                hipStream_t st, const BnIn *bn = nullptr, float2 *stats = nullptr) {
+                hipStream_t st, const BnIn *bn = nullptr, float2 *stats = nullptr, const BnGrad *bg = nullptr,
+                const GradStats *gs = nullptr) {
     const int cinp = round4(cin);
-    const size_t lds = ((size_t)cinp * kPlane + 2 * 2304 + (bn ? kBnStatFloats : 0)) * sizeof(float);
+    const size_t lds = ((size_t)cinp * kPlane + 2 * 2304 + (bn || bg ? kBnStatFloats : 0)) * sizeof(float);
     const int a = acc ? 1 : 0;
-    const BnIn none{};
-    const BnIn &b = bn ? *bn : none;
-    const int mode = (bn ? kBnIn : 0) | (stats ? kStatsOut : 0);
-    switch (cinp * 4 + mode) {
-    case 4 * 4 + 0: return launch_conv_t<4, 0>(B, lds, st, in, cin, wk, bias, cout, out, a, b, stats);
-    case 4 * 4 + kStatsOut: return launch_conv_t<4, kStatsOut>(B, lds, st, in, cin, wk, bias, cout, out, a, b, stats);
-    case 32 * 4 + 0: return launch_conv_t<32, 0>(B, lds, st, in, cin, wk, bias, cout, out, a, b, stats);
-    case 64 * 4 + 0: return launch_conv_t<64, 0>(B, lds, st, in, cin, wk, bias, cout, out, a, b, stats);
-    case 64 * 4 + kBnIn: return launch_conv_t<64, kBnIn>(B, lds, st, in, cin, wk, bias, cout, out, a, b, stats);
-    case 64 * 4 + (kBnIn | kStatsOut):
-        return launch_conv_t<64, kBnIn | kStatsOut>(B, lds, st, in, cin, wk, bias, cout, out, a, b, stats);
+    const BnIn bn0{};
+    const BnGrad bg0{};
+    const GradStats gs0{};
+    const BnIn &b = bn ? *bn : bn0;
+    const BnGrad &g = bg ? *bg : bg0;
+    const GradStats &s = gs ? *gs : gs0;
+    const int mode = (bn ? kBnIn : 0) | (stats ? kStatsOut : 0) | (bg ? kBnGrad : 0) | (gs ? kGradStats : 0);
+#define SPAI_CONV_CASE(C, M) \
+    case (C) * 16 + (M): return launch_conv_t<C, M>(B, lds, st, in, cin, wk, bias, cout, out, a, b, stats, g, s);
+    switch (cinp * 16 + mode) {
+    SPAI_CONV_CASE(4, 0)
+    SPAI_CONV_CASE(4, kStatsOut)
+    SPAI_CONV_CASE(4, kGradStats)
+    SPAI_CONV_CASE(32, 0)
+    SPAI_CONV_CASE(64, 0)
+    SPAI_CONV_CASE(64, kBnIn)
+    SPAI_CONV_CASE(64, kBnIn | kStatsOut)
+    SPAI_CONV_CASE(64, kBnGrad)
+    SPAI_CONV_CASE(64, kBnGrad | kGradStats)
     default: set_error("learner conv: %d input channels (mode %d) not built", cin, mode); return SPAI_ERR_UNSUPPORTED;
     }
+#undef SPAI_CONV_CASE
 }
 
-// dW, db of one conv: chunk partials on f32 MFMA, then a fixed-order sum over the chunks
-int launch_wgrad(float *wpart, const float *x, int cin, const float *dz, int cout, int B, float *dw, hipStream_t st) {
-    const int cinp = round4(cin), nk = (9 * cinp + 15) / 16, ntiles = (round16(cout) / 16) * nk;
+// dW (and db, when given) of one conv: chunk partials on f32 MFMA, then a fixed-order sum over the chunks
+int launch_wgrad(float *wpart, const float *x, int cin, const float *dz, int cout, int B, float *dw, hipStream_t st,
+                 float *db = nullptr) {
+    const int cinp = round4(cin), k1 = 9 * cinp + (db ? 1 : 0), nk = (k1 + 15) / 16, ntiles = (round16(cout) / 16) * nk;
     const int groups = std::max(1, (ntiles + 4 * kWgMaxTiles - 1) / (4 * kWgMaxTiles));
     const int chunks = (B + kWgSamples - 1) / kWgSamples;
-    const size_t lds = ((size_t)cinp * kPlane + (size_t)round16(cout) * 44) * sizeof(float);
+    const size_t lds = ((size_t)cinp * kPlane + (size_t)round16(cout) * 44 + (db ? kPlane : 0)) * sizeof(float);
     const dim3 grid(chunks, groups);
-    switch (cinp) {
-    case 4: k_wgrad_mfma<4><<<grid, kThreads, lds, st>>>(x, cin, dz, cout, B, groups, wpart); break;
-    case 64: k_wgrad_mfma<64><<<grid, kThreads, lds, st>>>(x, cin, dz, cout, B, groups, wpart); break;
+    switch (cinp * 2 + (db ? 1 : 0)) {
+    case 4 * 2: k_wgrad_mfma<4, false><<<grid, kThreads, lds, st>>>(x, cin, dz, cout, B, groups, wpart); break;
+    case 64 * 2: k_wgrad_mfma<64, false><<<grid, kThreads, lds, st>>>(x, cin, dz, cout, B, groups, wpart); break;
+    case 64 * 2 + 1: k_wgrad_mfma<64, true><<<grid, kThreads, lds, st>>>(x, cin, dz, cout, B, groups, wpart); break;
     default: set_error("learner wgrad: %d input channels not built", cin); return SPAI_ERR_UNSUPPORTED;
     }
-    k_wgrad_reduce<<<blocks_of((size_t)cout * 9 * cinp, kWgReduceThreads), kWgReduceThreads, 0, st>>>(wpart, chunks, cin,
-                                                                                                     cout, dw);
+    k_wgrad_reduce<<<blocks_of((size_t)cout * k1, kWgReduceThreads), kWgReduceThreads, 0, st>>>(wpart, chunks, cin, cout,
+                                                                                               dw, db);
     return SPAI_OK;
 }
 
@@ -1055,7 +1208,7 @@ void learner_destroy(spai_learner *L) {
     L->pack_desc.release();
     if (L->stage) (void)hipHostFree(L->stage);
     if (L->host_buf) (void)hipHostFree(L->host_buf);
-    for (auto *b : {&L->p, &L->g, &L->bsum, &L->m, &L->v, &L->wt, &L->batch_in, &L->d0, &L->d1, &L->bn_part, &L->dlogits,
+    for (auto *b : {&L->p, &L->g, &L->bsum, &L->m, &L->v, &L->wt, &L->batch_in, &L->d0, &L->d1, &L->d2, &L->dzb, &L->bn_part, &L->dlogits,
                     &L->dpre, &L->loss_terms, &L->run_buf})
         b->release();
     L->run_idx.release();
@@ -1174,7 +1327,9 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
 #define SPAI_WG_SIDE spai_learner::kWgStreams
 #endif
     int side = 0;
-    auto wgrad_async = [&](int l, const float *in) {
+    // dz: the layer's BN-backward output (z[l] overwritten by k_bn_bwd, or the fused
+    // path's dz buffer); db: the bias gradient from the weight gradient (fused path)
+    auto wgrad_async = [&](int l, const float *in, const float *dz = nullptr, float *db = nullptr) {
         const spai_learner::Conv &c = L->convs[l];
         if (crc != SPAI_OK) return;
         const int k = side++ % SPAI_WG_SIDE;
@@ -1184,7 +1339,8 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
             crc = SPAI_ERR_DEVICE;
             return;
         }
-        crc = launch_wgrad(L->wpart_side[k].p, in, c.ci, L->z[l].p, c.co, (int)B, G + c.w, L->wg_stream[k]);
+        crc = launch_wgrad(L->wpart_side[k].p, in, c.ci, dz ? dz : L->z[l].p, c.co, (int)B, G + c.w, L->wg_stream[k],
+                           db);
     };
     auto bn_conv_bwd = [&](int l, const float *da, const float *in, float *dx, bool acc, float *dy_out) {
         const spai_learner::Conv &c = L->convs[l];
@@ -1198,6 +1354,61 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
                                                                 G + L->val_w, G + L->val_b);
     k_linear_bwd_x<<<blocks_of((size_t)B * 3 * kCells), kThreads, 0, st>>>(L->dpre.p, P + L->val_w, (int)B, 1,
                                                                             3 * kCells, L->d1.p);
+    // SPAI_LEARNER_BNB_FUSE=0: a k_bn_bwd kernel before every data gradient (A/B knob);
+    // default (with the forward fusion): the trunk's BN backward runs in the data
+    // gradient's staging (BnGrad), its partials from the producer of da (GradStats)
+    static const bool bfuse = [] {
+        const char *v = std::getenv("SPAI_LEARNER_BNB_FUSE");
+        return !v || std::atoi(v) != 0;
+    }();
+    if (fuse && bfuse) {
+        const int last = 2 * L->blocks;
+        auto gpart_of = [&](int l) { return (float2 *)L->bn_part.p + (size_t)l * L->hidden * B; };
+        auto dzb_of = [&](int l) { return L->dzb.p + (size_t)(l - 1) * B * L->hidden * kCells; };   // l >= 1
+        auto gs_of = [&](int l) {
+            return GradStats{L->a[l].p, L->z[l].p, L->mean[l].p, L->invstd[l].p, gpart_of(l)};
+        };
+        auto bg_of = [&](int l, float *dy_out) {
+            const spai_learner::Conv &c = L->convs[l];
+            return BnGrad{gpart_of(l), L->a[l].p, L->z[l].p, L->mean[l].p, L->invstd[l].p, P + c.g, dzb_of(l), dy_out,
+                          G + c.g, G + c.be, (int)B};
+        };
+        {   // value head: its BN backward as before; its data gradient completes dL/d(trunk output)
+            const spai_learner::Conv &c = L->convs[val];
+            k_bn_bwd<<<c.co, kBn, 0, st>>>(L->d1.p, L->a[val].p, L->z[val].p, c.co, (int)B, L->mean[val].p,
+                                           L->invstd[val].p, P + c.g, G + c.g, G + c.be, G + c.b, L->z[val].p, nullptr);
+            wgrad_async(val, h);
+            const GradStats g = gs_of(last);
+            if (crc == SPAI_OK)
+                crc = launch_conv(L->z[val].p, c.co, W + c.wkd, nullptr, c.ci, L->d0.p, (int)B, true, st, nullptr,
+                                  nullptr, nullptr, last > 0 ? &g : nullptr);
+        }
+        float *X = L->d0.p, *Y = L->d1.p, *T = L->d2.p;   // dL/d(block output), dL/d(relu1 output), skip + block input
+        for (int k = L->blocks - 1; k >= 0 && crc == SPAI_OK; --k) {
+            const int l1 = 1 + 2 * k, l2 = 2 + 2 * k;
+            const float *hin = L->a[l1 - 1].p;
+            {   // conv 2: dz from X (dy = the skip gradient -> T), dx -> Y, the partials of conv 1's BN
+                const spai_learner::Conv &c = L->convs[l2];
+                const BnGrad bgv = bg_of(l2, T);
+                const GradStats g = gs_of(l1);
+                crc = launch_conv(X, c.co, W + c.wkd, nullptr, c.ci, Y, (int)B, false, st, nullptr, nullptr, &bgv, &g);
+                wgrad_async(l2, L->a[l1].p, dzb_of(l2), G + c.b);
+            }
+            if (crc == SPAI_OK) {   // conv 1: dz from Y, dx accumulated into T = dL/d(block input)
+                const spai_learner::Conv &c = L->convs[l1];
+                const BnGrad bgv = bg_of(l1, nullptr);
+                const GradStats g = gs_of(l1 - 1);
+                crc = launch_conv(Y, c.co, W + c.wkd, nullptr, c.ci, T, (int)B, true, st, nullptr, nullptr, &bgv,
+                                  l1 - 1 > 0 ? &g : nullptr);
+                wgrad_async(l1, hin, dzb_of(l1), G + c.b);
+            }
+            float *nx = T;
+            T = Y;
+            Y = X;
+            X = nx;
+        }
+        bn_conv_bwd(0, X, x_in, nullptr, false, nullptr);   // stem: no data gradient
+    } else {
     bn_conv_bwd(val, L->d1.p, h, L->d0.p, true, nullptr);
     // residual blocks in reverse; d0 holds dL/d(block output)
     for (int k = L->blocks - 1; k >= 0; --k) {
@@ -1214,6 +1425,7 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
     }
     // stem: no data gradient
     bn_conv_bwd(0, L->d0.p, x_in, nullptr, false, nullptr);
+    }
     // join: every weight gradient is in G before the reduction and Adam
     for (int k = 0; k < SPAI_WG_SIDE && crc == SPAI_OK; ++k)
         if (hipEventRecord(L->ev_wg_done[k], L->wg_stream[k]) != hipSuccess ||

@@ -159,7 +159,10 @@ struct spai_learner {
     float *stage = nullptr;             // pinned host copy of it, then the loss terms [B*2]
     std::vector<spai::DevBuf<float>> z, a, mean, invstd;   // per conv layer
     spai::DevBuf<float> d0, d1;         // backward scratch [B][64][42]
-    spai::DevBuf<float> bn_part;        // trunk convs' BN partials [layer][64][B] x {sum, centred sum of squares}
+    spai::DevBuf<float> bn_part;        // trunk convs' BN partials [layer][64][B] x 2 (forward: sum, centred sum
+                                        // of squares; backward: sum dy, sum dy xhat)
+    spai::DevBuf<float> dzb, d2;        // fused BN backward: dz of the trunk convs [2 blocks][B][64][42]; a third
+                                        // activation-gradient buffer
     spai::DevBuf<float> dlogits, dpre, loss_terms;
     spai::DevBuf<uint32_t> run_idx;     // BN running-stat offsets (for the cross-rank average)
     spai::DevBuf<float> run_buf;
