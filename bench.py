@@ -432,11 +432,19 @@ def main():
             ms = net.bench(n, iters=300)
             tf = fpe * n / (ms * 1e-3) / 1e12
             iso[str(n)] = {"ms": ms, "TFLOP/s": tf, "frac": tf / BF16_PEAK_TFLOPS}
+        # the timed region's configuration: a chain's forward at the mean leaves with the
+        # group size the search picks for two chains sharing the CUs (group_size_conc)
+        n = max(1, mean_leaves)
+        ms = net.bench(n, iters=300, conc=2)
+        tf = fpe * n / (ms * 1e-3) / 1e12
+        iso["%d@conc2" % n] = {"ms": ms, "TFLOP/s": tf, "frac": tf / BF16_PEAK_TFLOPS}
         result["roofline"]["isolated"] = iso
         result["roofline"]["isolated_note"] = ("k_forward alone on the GPU at N leaves per launch (spai_net_bench: "
                                                "300 back-to-back launches between HIP events, after ~0.2 s of "
-                                               "warm-up launches); the timed region's per-launch figure shares the "
-                                               "CUs with the other search chain")
+                                               "warm-up launches) at the one-chain group size; 'N@conc2' at the "
+                                               "group size the timed region's two chains use (spai_net_bench_conc); "
+                                               "the timed region's per-launch figure shares the CUs with the other "
+                                               "search chain")
     if not args.no_rules_bench and dist.rank == 0:
         result["rules_kernels"] = rules_bench(eng)
     net.close()

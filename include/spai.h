@@ -220,6 +220,10 @@ int spai_net_phase_cycles(spai_net *net, uint32_t count, double *cycles);
  * ms = mean over `iters` back-to-back launches on `count` random reachable
  * positions, HIP events on the engine stream.  Measurement only. */
 int spai_net_bench(spai_net *net, uint32_t count, uint32_t iters, double *ms);
+/* the same with the group size the search picks when `conc` search chains'
+ * forwards share the CUs (conc 1 = spai_net_bench): the timed region's
+ * configuration of a chain's forward, measured alone */
+int spai_net_bench_conc(spai_net *net, uint32_t count, uint32_t iters, int conc, double *ms);
 
 /* ---------------------------------------------------------------- learner
  * The training step of the C4 net on the device:

@@ -390,6 +390,17 @@ int spai_net_bench(spai_net *n, uint32_t count, uint32_t iters, double *ms) {
     return net_bench(n, count, iters, ms);
 }
 
+int spai_net_bench_conc(spai_net *n, uint32_t count, uint32_t iters, int conc, double *ms) {
+    PTR_CHECK(n);
+    PTR_CHECK(ms);
+    ENG_CHECK(n->eng);
+    if (conc < 1) {
+        set_error("conc %d < 1", conc);
+        return SPAI_ERR_INVALID;
+    }
+    return net_bench(n, count, iters, ms, conc);
+}
+
 int spai_engine_timing_items(spai_engine *e, double *total_ms, double *items) {
     ENG_CHECK(e);
     for (int i = 0; i < 3; ++i) {

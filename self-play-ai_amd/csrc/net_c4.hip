@@ -1590,7 +1590,7 @@ static void random_positions(uint32_t cnt, std::vector<uint64_t> &m, std::vector
 // Device time of the search's forward launch alone (net_eval_batch with a
 // device-side leaf count, as in search) on `cnt` random positions: mean of
 // `iters` back-to-back launches between two HIP events on the engine stream.
-int net_bench(spai_net *n, uint32_t cnt, uint32_t iters, double *ms) {
+int net_bench(spai_net *n, uint32_t cnt, uint32_t iters, double *ms, int conc) {
     SPAI_CHECK(cnt > 0 && iters > 0, SPAI_ERR_INVALID, "need cnt > 0 and iters > 0");
     SPAI_TRY(ensure_io(n, cnt));
     if (!n->io_count.p) SPAI_TRY(n->io_count.alloc(1));
@@ -1601,13 +1601,15 @@ int net_bench(spai_net *n, uint32_t cnt, uint32_t iters, double *ms) {
     SPAI_HIP(hipMemcpyAsync(n->io_theirs.p, t.data(), (size_t)cnt * 8, hipMemcpyHostToDevice, st));
     SPAI_HIP(hipMemcpyAsync(n->io_count.p, &cnt, 4, hipMemcpyHostToDevice, st));
     for (int w = 0; w < 3; ++w)
-        SPAI_TRY(net_eval_batch(n, st, n->io_count.p, cnt, n->io_mine.p, n->io_theirs.p, n->io_priors.p, n->io_value.p));
+        SPAI_TRY(net_eval_batch(n, st, n->io_count.p, cnt, n->io_mine.p, n->io_theirs.p, n->io_priors.p, n->io_value.p,
+                                0, conc));
     hipEvent_t a, b;
     SPAI_HIP(hipEventCreate(&a));
     SPAI_HIP(hipEventCreate(&b));
     SPAI_HIP(hipEventRecord(a, st));
     for (uint32_t i = 0; i < iters; ++i)
-        SPAI_TRY(net_eval_batch(n, st, n->io_count.p, cnt, n->io_mine.p, n->io_theirs.p, n->io_priors.p, n->io_value.p));
+        SPAI_TRY(net_eval_batch(n, st, n->io_count.p, cnt, n->io_mine.p, n->io_theirs.p, n->io_priors.p, n->io_value.p,
+                                0, conc));
     SPAI_HIP(hipEventRecord(b, st));
     SPAI_HIP(hipEventSynchronize(b));
     float f = 0;

@@ -241,7 +241,7 @@ int net_forward_x(spai_net *net, uint32_t n, const float *x, float *logits, floa
 int net_predict(spai_net *net, uint32_t n, const spai_c4_state *states, float *priors, float *values);
 size_t net_num_params(int game, int blocks, int hidden);
 int net_phase_stamps(spai_net *net, uint32_t n, double *cycles);
-int net_bench(spai_net *net, uint32_t n, uint32_t iters, double *ms);
+int net_bench(spai_net *net, uint32_t n, uint32_t iters, double *ms, int conc = 1);
 void net_init_params(int game, int blocks, int hidden, uint64_t seed, float *params);
 // evaluate `count` (device scalar) leaves of the batch; grid sized for max_n; conc:
 // search chains whose forwards share the CUs (the group-size policy, net_c4.hip)

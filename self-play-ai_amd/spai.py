@@ -33,7 +33,7 @@ SYMBOLS = [
     "spai_net_destroy", "spai_net_forward", "spai_predict", "spai_engine_set_net", "spai_trees_create",
     "spai_tree_reset", "spai_search", "spai_tree_use_subtree", "spai_tree_node", "spai_tree_size",
     "spai_selfplay_run", "spai_engine_set_timing", "spai_engine_timing", "spai_engine_timing_items",
-    "spai_net_phase_cycles", "spai_net_bench", "spai_adam_config_default", "spai_learner_create", "spai_learner_destroy",
+    "spai_net_phase_cycles", "spai_net_bench", "spai_net_bench_conc", "spai_adam_config_default", "spai_learner_create", "spai_learner_destroy",
     "spai_learner_train_batch", "spai_learner_params", "spai_learner_grads", "spai_learner_activation", "spai_comm_unique_id",
     "spai_learner_set_comm", "spai_learner_broadcast", "spai_learner_set_host_comm", "spai_learner_last_batch",
     "spai_comm_create", "spai_comm_allreduce_f64", "spai_comm_info", "spai_comm_destroy",
@@ -167,6 +167,7 @@ def lib():
         L.spai_engine_timing_items.argtypes = [vp, vp, vp]
         L.spai_net_phase_cycles.argtypes = [vp, u32, vp]
         L.spai_net_bench.argtypes = [vp, u32, u32, vp]
+        L.spai_net_bench_conc.argtypes = [vp, u32, u32, i32, vp]
         L.spai_adam_config_default.argtypes = [P(AdamConfig)]
         L.spai_learner_create.argtypes = [vp, i32, i32, vp, C.c_size_t, P(AdamConfig), P(vp)]
         L.spai_learner_destroy.argtypes = [vp]
@@ -271,10 +272,11 @@ class Net:
         _check(lib().spai_net_phase_cycles(self.h, count, _p(c)))
         return c
 
-    def bench(self, count, iters=50):
-        """ms per forward launch alone on `count` random positions (spai_net_bench)"""
+    def bench(self, count, iters=50, conc=1):
+        """ms per forward launch alone on `count` random positions (spai_net_bench); conc > 1:
+        at the group size the search picks for conc concurrent chains (spai_net_bench_conc)"""
         ms = np.zeros(1, np.float64)
-        _check(lib().spai_net_bench(self.h, count, iters, _p(ms)))
+        _check(lib().spai_net_bench_conc(self.h, count, iters, conc, _p(ms)))
         return float(ms[0])
 
     def predict(self, states):
