@@ -293,15 +293,37 @@ def spawn_ranks(n):
     return failed[0] if failed and failed[0] > 0 else 1
 
 
+class _StdoutToStderr:
+    """C-level stdout (fd 1) to stderr for a block: RCCL prints its version banner
+    to stdout at communicator creation, and rank 0's stdout must hold exactly one
+    JSON line"""
+
+    def __enter__(self):
+        import ctypes
+        self.libc = ctypes.CDLL(None)
+        sys.stdout.flush()
+        self.libc.fflush(None)
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        self.libc.fflush(None)
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+        return False
+
+
 def rccl_comm(dist, spai):
     """an RCCL communicator over the ranks' devices (rank 0's id through the host
     group); None with a reason when the ranks share a device (RCCL refuses that)"""
     devs = dist.g.allgather(dist.local)
     if len(set(devs)) != len(devs):
         return None, "ranks share device(s) %s: RCCL needs one rank per GPU; host group only" % devs
-    uid = dist.g.broadcast_bytes(spai.comm_unique_id() if dist.rank == 0 else None)
     try:
-        return spai.Comm(dist.local, dist.rank, dist.world, uid), None
+        with _StdoutToStderr():
+            uid = dist.g.broadcast_bytes(spai.comm_unique_id() if dist.rank == 0 else None)
+            return spai.Comm(dist.local, dist.rank, dist.world, uid), None
     except Exception as ex:   # reported in the line; the host group still carries the reductions
         return None, "RCCL communicator failed: %r" % (ex,)
 
@@ -355,13 +377,15 @@ def main():
     rccl = {"ranks": 0, "note": comm_note}
     if comm is not None:   # the same reductions over RCCL (xGMI between GPUs): exact for these integer counts
         try:
-            r_sum = comm.allreduce(counters, "sum")
-            (r_max,) = comm.allreduce([dt], "max")
+            with _StdoutToStderr():
+                r_sum = comm.allreduce(counters, "sum")
+                (r_max,) = comm.allreduce([dt], "max")
             rccl = {"ranks": comm.info()[1], "devices": dist.g.allgather(dist.local),
                     "counters_agree": r_sum == [sims, games, evals, positions] and r_max == dt_max}
         except Exception as ex:
             rccl = {"ranks": 0, "note": "RCCL all-reduce failed: %r" % (ex,)}
-        comm.close()
+        with _StdoutToStderr():
+            comm.close()
 
     fpe = flops_per_eval(args.blocks)
     ev = timing["evaluate"]

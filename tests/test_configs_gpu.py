@@ -179,8 +179,8 @@ def test_bench_gpus_flag_spawns_ranks():
         p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(gpus),
                             "--games", str(games)] + args, env=env, capture_output=True, text=True, timeout=240)
         assert p.returncode == 0, p.stderr[-3000:]
-        lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
-        assert len(lines) == 1, p.stdout[-2000:]   # rank 0's line only
+        lines = p.stdout.splitlines()
+        assert len(lines) == 1 and lines[0].startswith("{"), p.stdout[-2000:]   # rank 0's one JSON line, nothing else
         return json.loads(lines[0])
 
     one, two = run(1, 2 * G), run(2, G)
