@@ -11,11 +11,11 @@ if [ -z "$SKIP_TESTS" ]; then
   rc=$?; tail -3 $O/pytest_chess.log; echo "pytest rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
 for r in 1 2; do
-  for L in build_exp/libspai_chessold.so self-play-ai_amd/libspai.so; do
+  for L in build_exp/libspai_chessold.so self-play-ai_amd/libspai.so ${CHESS_EXTRA:-build_exp/libspai_chessfixw.so}; do
     n=$(basename $L .so)_$r
     SPAI_LIB=$L timeout -k 10 300 python3 scripts/chess_bench.py --moves 2 --no-cpu-baseline > $O/chess_$n.json 2> $O/chess_$n.err
     rc=$?; [ $rc -eq 0 ] || { tail -5 $O/chess_$n.err; exit $rc; }
-    python3 -c "import json; d=json.load(open('$O/chess_$n.json')); print('$n', round(d['value']), d['roofline']['avg_launch_ms'] if 'avg_launch_ms' in d['roofline'] else '', round(d['roofline']['frac'],4))"
+    python3 -c "import json; d=json.loads([l for l in open('$O/chess_$n.json') if l.startswith('{')][-1]); print('$n', round(d['value']), d['roofline']['avg_launch_ms'] if 'avg_launch_ms' in d['roofline'] else '', round(d['roofline']['frac'],4))"
   done
 done
 for c in FETCH_SIZE WRITE_SIZE; do

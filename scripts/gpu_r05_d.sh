@@ -11,9 +11,10 @@ if [ -z "$SKIP_TESTS" ]; then
   rc=$?; grep -E "PASS|FAIL|ERROR|passed|failed" $O/pytest_learner.log | tail -15; echo "pytest rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
 for r in 1 2; do
-  for f in 0 1; do
-    SPAI_LEARNER_BN_FUSE=$f timeout -k 10 200 python scripts/learner_dp.py --steps 300 > $O/learner_f${f}_$r.json 2> $O/learner_f${f}_$r.err || { tail -3 $O/learner_f${f}_$r.err; exit 1; }
-    python3 -c "import json;d=json.load(open('$O/learner_f${f}_$r.json'));print('fuse=$f', round(d['value']), 'samples/s', round(d['ms_per_step'],4), 'ms/step')"
+  for v in SPAI_LEARNER_BN_FUSE=0 SPAI_LEARNER_BNB_FUSE=0 SPAI_LEARNER_BN_FUSE=1; do
+    n=$(echo $v | tr '=' '_')_$r
+    env $v timeout -k 10 200 python scripts/learner_dp.py --steps 300 > $O/learner_$n.json 2> $O/learner_$n.err || { tail -3 $O/learner_$n.err; exit 1; }
+    python3 -c "import json;d=json.loads([l for l in open('$O/learner_$n.json') if l.startswith('{')][-1]);print('$n', round(d['value']), 'samples/s', round(d['ms_per_step'],4), 'ms/step')"
   done
 done
 rm -rf /tmp/lprof

@@ -303,7 +303,11 @@ __device__ __forceinline__ void forward_body(uint8_t *smem, uint32_t count, uint
     epilogue<false, NT>(smem, kBufA, wave, lane, acc);
     __syncthreads();
     for (int l = 0; l < W.blocks; ++l) {
+#ifdef SPAI_CHESS_EXP_FIXW   // timing experiment (wrong results): every block reads block 0's weights (L2-resident)
+        const size_t l1 = 0, l2 = 1;
+#else
         const size_t l1 = 2 * l, l2 = 2 * l + 1;
+#endif
         conv<9, 8, NT>(smem, kBufA, W.w_res + l1 * 72 * kCT * kFrag, W.b_res + l1 * kHid, wave, lane, acc);
         epilogue<false, NT>(smem, kBufB, wave, lane, acc);
         __syncthreads();
