@@ -107,10 +107,30 @@ __device__ __forceinline__ int row_chunk(int v, int c) { return v * kStride + (c
 #ifndef SPAI_CHESS_TAP_UNROLL
 #define SPAI_CHESS_TAP_UNROLL 9   // taps per iteration of the tap loop (9: fully unrolled, 1.92 vs 1.99 ms)
 #endif
+// SPAI_CHESS_PREFETCH (experiment): at a conv's start every wave loads its
+// share of the NEXT conv's weight fragments (the 128 waves of an XCD split the
+// layer's 72 x 16 fragments), so that layer's ring loads hit the XCD's L2
+// instead of going to the Infinity Cache one k-step window ahead; the loads'
+// values feed a never-taken store, so they are waited for once, early in this conv.
 template <int TAPS, int CB, int NT>
 __device__ __forceinline__ void conv(const uint8_t *smem, int in, const uint4 *__restrict__ w,
-                                     const float *__restrict__ bias, int wave, int lane, f32x4 (&acc)[kCPW][NT]) {
+                                     const float *__restrict__ bias, int wave, int lane, f32x4 (&acc)[kCPW][NT],
+                                     const uint4 *__restrict__ wnext = nullptr, float *__restrict__ sink = nullptr) {
     constexpr int DA = SPAI_CHESS_DA;
+#ifdef SPAI_CHESS_PREFETCH
+    uint32_t pf = 0;
+    if (wnext) {
+        const int g = (int)((blockIdx.x >> 3) & 31u) * kWaves + wave;   // blocks b, b + 8, ... share an XCD
+#pragma unroll
+        for (int j = 0; j < (72 * kCT + 127) / 128; ++j) {
+            const int f = g + 128 * j;
+            if (f < 72 * kCT) pf ^= wnext[(size_t)f * kFrag + lane].x;
+        }
+    }
+#else
+    (void)wnext;
+    (void)sink;
+#endif
     const int q = lane >> 4, col = lane & 15;
     f32x4 bv[kCPW];
 #pragma unroll
@@ -210,6 +230,9 @@ __device__ __forceinline__ void conv(const uint8_t *smem, int in, const uint4 *_
                                                                         as_bf16x8(B[ks & 1][t]), acc[c][t], 0, 0, 0);
         }
     }
+#ifdef SPAI_CHESS_PREFETCH
+    if (wnext && pf == 0x9E3779B9u && acc[0][0][0] == -1234.5678f) sink[lane] = (float)pf;   // never taken
+#endif
 }
 
 // relu(acc [+ residual at OUT]) -> bf16 at OUT (in place over the residual)
@@ -308,10 +331,12 @@ __device__ __forceinline__ void forward_body(uint8_t *smem, uint32_t count, uint
 #else
         const size_t l1 = 2 * l, l2 = 2 * l + 1;
 #endif
-        conv<9, 8, NT>(smem, kBufA, W.w_res + l1 * 72 * kCT * kFrag, W.b_res + l1 * kHid, wave, lane, acc);
+        conv<9, 8, NT>(smem, kBufA, W.w_res + l1 * 72 * kCT * kFrag, W.b_res + l1 * kHid, wave, lane, acc,
+                       W.w_res + l2 * 72 * kCT * kFrag, value);
         epilogue<false, NT>(smem, kBufB, wave, lane, acc);
         __syncthreads();
-        conv<9, 8, NT>(smem, kBufB, W.w_res + l2 * 72 * kCT * kFrag, W.b_res + l2 * kHid, wave, lane, acc);
+        conv<9, 8, NT>(smem, kBufB, W.w_res + l2 * 72 * kCT * kFrag, W.b_res + l2 * kHid, wave, lane, acc,
+                       l + 1 < W.blocks ? W.w_res + (l2 + 1) * 72 * kCT * kFrag : nullptr, value);
         if (SPAI_CHESS_RES_MFMA) {
             residual_mfma<NT>(smem, kBufA, wave, lane, acc);
             epilogue<false, NT>(smem, kBufA, wave, lane, acc);
