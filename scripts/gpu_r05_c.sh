@@ -11,7 +11,7 @@ if [ -z "$SKIP_TESTS" ]; then
   rc=$?; tail -3 $O/pytest_chess.log; echo "pytest rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
 for r in 1 2; do
-  for L in build_exp/libspai_chessold.so self-play-ai_amd/libspai.so ${CHESS_EXTRA:-build_exp/libspai_chessfixw.so build_exp/libspai_chesspf.so}; do
+  for L in build_exp/libspai_chessold.so self-play-ai_amd/libspai.so ${CHESS_EXTRA:-build_exp/libspai_chesspf.so}; do
     n=$(basename $L .so)_$r
     SPAI_LIB=$L timeout -k 10 300 python3 scripts/chess_bench.py --moves 2 --no-cpu-baseline > $O/chess_$n.json 2> $O/chess_$n.err
     rc=$?; [ $rc -eq 0 ] || { tail -5 $O/chess_$n.err; exit $rc; }
