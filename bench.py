@@ -83,7 +83,7 @@ def parse():
     ap.add_argument("--cpu-games", type=int, default=100,
                     help="games the CPU baseline plays to completion inside this run: the reference worker's batch "
                          "(learner_concurrent.rs:50-59, num_batched_self_play_games = 100), ~2 min on the GPU box's host")
-    ap.add_argument("--cpu-timeout", type=float, default=480.0)
+    ap.add_argument("--cpu-timeout", type=float, default=360.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-rules-bench", action="store_true", help="skip the batched rules-kernel timing (HBM GB/s)")
     ap.add_argument("--no-chess", action="store_true", help="skip the chess window (config 4, 2 moves)")
