@@ -737,3 +737,51 @@ def test_self_play_sampling_frequencies(spai):
     for t_alt in (1.0, 1.5):
         c_alt, p_alt, _, _ = rank_chi2(pol, mv, t_alt)
         assert p_alt < 1e-12, (t_alt, c_alt, p_alt)
+
+
+def test_learner_bn_fusion_matches_unfused(spai, tmp_path):
+    """the trunk's BatchNorm forward (BnIn) and backward (BnGrad) run inside the
+    neighbouring convs by default; SPAI_LEARNER_BN_FUSE=0 keeps one k_bn_fwd /
+    k_bn_bwd kernel per conv (read once per process, hence the subprocess).  Two
+    Adam steps at 6 blocks x batch 128 from the same data: the two paths differ
+    only in the summation order of the batch statistics (Chan's merge of
+    per-sample partials against one two-pass sum), so losses agree to 1e-5
+    relative, the median parameter to 1e-6 and every parameter within lr per
+    step (Adam's g / (|g| + eps) can turn a rounding-level gradient difference
+    into a step of up to lr, e.g. on the biases of the convs that feed a
+    BatchNorm, whose gradient is rounding noise either way)"""
+    import json
+    import subprocess
+    import sys
+    from conftest import REPO
+    B, blocks, steps = 128, 6, 2
+    states = _reachable_positions(spai, 4 * B, 12, seed=3)[:B * steps]
+    e = spai.Engine(num_searches=1, max_trees=1)
+    e.games_resize(len(states))
+    e.games_write(states)
+    x = e.encode(len(states)).reshape(len(states), 126)
+    e.close()
+    rng = np.random.default_rng(5)
+    pi = rng.random((len(x), 7)).astype(np.float32) ** 2
+    pi = (pi / pi.sum(1, keepdims=True)).astype(np.float32)
+    z = rng.choice(np.array([-1, 0, 1], np.float32), len(x))
+    np.savez(tmp_path / "batch.npz", x=x, pi=pi, z=z)
+    code = (
+        "import sys, numpy as np; sys.path.insert(0, %r); import spai\n"
+        "d = np.load(%r); e = spai.Engine(num_searches=1, max_trees=1)\n"
+        "L = spai.Learner(e, %d, spai.init_params(%d, 64, seed=11))\n"
+        "loss = [L.train_batch(d['x'][k*%d:(k+1)*%d], d['pi'][k*%d:(k+1)*%d], d['z'][k*%d:(k+1)*%d]) for k in range(%d)]\n"
+        "np.savez(sys.argv[1], loss=np.array(loss), p=L.params())\n"
+        % (os.path.join(REPO, "self-play-ai_amd"), str(tmp_path / "batch.npz"), blocks, blocks, B, B, B, B, B, B, steps))
+    out = {}
+    for fuse in ("1", "0"):
+        f = str(tmp_path / ("out%s.npz" % fuse))
+        r = subprocess.run([sys.executable, "-c", code, f], env=dict(os.environ, SPAI_LEARNER_BN_FUSE=fuse),
+                           capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[fuse] = np.load(f)
+    np.testing.assert_allclose(out["1"]["loss"], out["0"]["loss"], rtol=1e-5, atol=1e-6)
+    p1, p0 = out["1"]["p"], out["0"]["p"]
+    d = np.abs(p1 - p0)
+    assert d.max() <= 2 * steps * 1e-3, d.max()
+    assert np.median(d) <= 1e-6, np.median(d)   # the bulk of the parameters moves identically
