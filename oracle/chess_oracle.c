@@ -863,7 +863,7 @@ long orc_self_play(int n_games, int num_searches, float c, float temperature, ui
         for (int k = n_act - 1; k >= 0; --k) {
             orc_game *sg = &g[idx[k]];
             orc_tree *t = sg->tree;
-            double u = or_uniform(seed, game_id_base + (uint64_t)sg->index, (uint64_t)move_no);
+            float u = or_u01_f32(seed, game_id_base + (uint64_t)sg->index, (uint64_t)move_no);
             int pick = or_weighted_index(rvis + (size_t)k * ORC_MAX_MOVES, rnc[k], temperature, u);
             if (pick < 0) { rc = -4; goto done; }
             int sel = rids[(size_t)k * ORC_MAX_MOVES + pick];

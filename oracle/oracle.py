@@ -62,9 +62,9 @@ def lib():
         L.or_encode_states.argtypes = [i, i, C.POINTER(vp), fp]
         L.or_ttt_init.argtypes = [vp]
         L.or_ttt_next_state.argtypes = [vp, i, vp]
-        L.or_uniform.restype = d
-        L.or_uniform.argtypes = [u64, u64, u64]
-        L.or_weighted_index.argtypes = [fp, i, f, d]
+        L.or_u01_f32.restype = f
+        L.or_u01_f32.argtypes = [u64, u64, u64]
+        L.or_weighted_index.argtypes = [fp, i, f, f]
         L.or_policy_best_action.argtypes = [fp, i]
         L.or_policy_sample.argtypes = [fp, i, f, f]
         L.or_splitmix64.restype = u64

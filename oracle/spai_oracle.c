@@ -325,36 +325,24 @@ void or_philox4x32(uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-double or_uniform(uint64_t seed, uint64_t game_id, uint64_t move_no) {
+/* rand 0.8's UniformFloat<f32> draw from the counter-based stream: the top 23
+ * bits of the first Philox word as a float in [1, 2), minus 1 */
+float or_u01_f32(uint64_t seed, uint64_t game_id, uint64_t move_no) {
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
     uint32_t ctr[4] = {(uint32_t)move_no, (uint32_t)(move_no >> 32), (uint32_t)game_id, (uint32_t)(game_id >> 32)};
     uint32_t out[4];
     or_philox4x32(ctr, key, out);
-    uint64_t bits = ((uint64_t)out[0] << 21) ^ ((uint64_t)out[1] >> 11);  /* 53 bits */
-    bits &= (1ull << 53) - 1;
-    return (double)bits * (1.0 / 9007199254740992.0);
+    uint32_t b = (out[0] >> 9) | 0x3F800000u;
+    float f;
+    memcpy(&f, &b, 4);
+    return f - 1.0f;
 }
 
-/* WeightedIndex over visit^temperature (learner_concurrent.rs:189-193).
- * Weights and their running sum are kept in double; the index is the first
- * one whose cumulative weight exceeds u * total. */
-int or_weighted_index(const float *visits, int n, float temperature, double u) {
-    double cum[512];
-    double total = 0.0;
-    if (n <= 0 || n > 512) return -1;
-    for (int i = 0; i < n; ++i) {
-        double w = pow((double)visits[i], (double)temperature);
-        total += w;
-        cum[i] = total;
-    }
-    if (!(total > 0.0)) return -2;  /* WeightedIndex::new(..).unwrap() panics */
-    double x = u * total;
-    int last = 0;  /* WeightedIndex never returns a zero-weight item: fall back to the last nonzero one */
-    for (int i = 0; i < n; ++i) {
-        if (cum[i] > x) return i;
-        if (i == 0 ? cum[0] > 0.0 : cum[i] > cum[i - 1]) last = i;
-    }
-    return last;
+/* the self-play move draw (learner_concurrent.rs:189-193): WeightedIndex<f32> over
+ * (visit_count as f32).powf(temperature), i.e. Policy::sample's arithmetic on the
+ * child visit counts (or_policy_sample below); -1 when the reference panics */
+int or_weighted_index(const float *visits, int n, float temperature, float u01) {
+    return or_policy_sample(visits, n, temperature, u01);
 }
 
 /* Policy::get_best_action (connect_four.rs:116-124): Iterator::max_by with
@@ -999,7 +987,7 @@ long or_self_play(int game, int n_games, int num_searches, float c, float temper
             sp_game *sg = &games[act_idx[k]];
             or_tree *t = sg->tree;
             int nc = rnc[k];
-            double u = or_uniform(seed, game_id_base + (uint64_t)sg->game_index, (uint64_t)move_no);
+            float u = or_u01_f32(seed, game_id_base + (uint64_t)sg->game_index, (uint64_t)move_no);
             int idx = or_weighted_index(rvis + (size_t)k * A, nc, temperature, u);
             if (idx < 0) { rc = -4; goto done; }
             int selected = rids[(size_t)k * A + idx];

@@ -98,8 +98,8 @@ int or_ttt_next_state(const or_ttt_state *s, int action, or_ttt_state *out);
 /* ---- Philox4x32-10 + sampling (deterministic restatement of the unseeded
  *      rand::thread_rng + WeightedIndex, learner_concurrent.rs:189-193) ---- */
 void or_philox4x32(uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
-double or_uniform(uint64_t seed, uint64_t game_id, uint64_t move_no);
-int or_weighted_index(const float *visits, int n, float temperature, double u);
+float or_u01_f32(uint64_t seed, uint64_t game_id, uint64_t move_no);
+int or_weighted_index(const float *visits, int n, float temperature, float u01);
 /* Policy::get_best_action / Policy::sample on a flat policy (game/mod.rs:42-43) */
 int or_policy_best_action(const float *p, int n);
 int or_policy_sample(const float *p, int n, float temperature, float u01);

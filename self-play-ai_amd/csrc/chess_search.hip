@@ -836,7 +836,7 @@ int selfplay_run(spai_chess *e, uint32_t n_games, uint64_t gid_base, spai_chess_
             const uint32_t *vis = Tr.h_visits.data() + (size_t)k * kMaxMoves;
             float fv[kMaxMoves];
             for (uint32_t j = 0; j < nch; ++j) fv[j] = (float)vis[j];
-            const double u = sample_uniform(e->cfg.seed, gid_base + t, move_no);
+            const float u = sample_u01_f32(e->cfg.seed, gid_base + t, move_no);
             const int idx = weighted_index(fv, (int)nch, e->cfg.temperature, u);
             SPAI_CHECK(idx >= 0, SPAI_ERR_NAN, "WeightedIndex over all-zero visits (the reference panics)");
             pick[k] = (uint32_t)idx;

@@ -4,9 +4,10 @@
 // WeightedIndex over visit_count^temperature (learner_concurrent.rs:177,189-193),
 // which is unseeded.  Here the uniform comes from Philox4x32-10 keyed by
 // (seed, game id, move number), so a game's trajectory does not depend on how
-// games are batched or sharded across GPUs; the weights and their running sum
-// are kept in double.  oracle/spai_oracle.c (or_uniform, or_weighted_index)
-// restates the same definition for the parity tests.
+// games are batched or sharded across GPUs; the weights, their running sum and
+// the draw follow rand 0.8's WeightedIndex<f32> exactly (f32 arithmetic).
+// oracle/spai_oracle.c (or_u01_f32, or_policy_sample) restates the same
+// definition for the parity tests.
 #pragma once
 #include <stdint.h>
 
@@ -45,52 +46,51 @@ SPAI_PHX double sample_uniform(uint64_t seed, uint64_t game_id, uint64_t move_no
     return (double)bits * (1.0 / 9007199254740992.0);
 }
 
-// index of the sampled child, -1 if n is out of range, -2 if all weights are 0
-// visits^temperature for the integer visit counts of a self-play run, each
-// computed once by the same std::pow (so the weights are the same bits); any
-// other value goes to std::pow directly
-struct PowCache {
-    double temperature = -1.0;
-    std::vector<double> tab;
-    double operator()(float v, float t) {
-        if ((double)t != temperature) {
-            temperature = (double)t;
-            tab.clear();
-        }
-        if (!(v >= 0.f) || v >= 1.0e6f || v != (float)(uint32_t)v) return std::pow((double)v, (double)t);
-        const uint32_t k = (uint32_t)v;
-        while (tab.size() <= k) tab.push_back(std::pow((double)tab.size(), (double)t));
-        return tab[k];
-    }
-};
-
-// the sampled index from the running sums cum[0..n) of the weights (total = cum[n-1])
-SPAI_PHX int weighted_index_cum(const double *cum, int n, double total, double u) {
-    if (!(total > 0.0)) return -2;
-    double x = u * total;
-    int last = 0;   // last index whose cumulative weight increased (rand never picks a zero weight)
-    for (int i = 0; i < n; ++i) {
-        if (cum[i] > x) return i;
-        if (i == 0 ? cum[0] > 0.0 : cum[i] > cum[i - 1]) last = i;
-    }
-    return last;   // u * total rounded up to total
+// rand 0.8's UniformFloat<f32> draw (Uniform::new(0, total).sample): the top 23
+// bits of a Philox word as a float in [1, 2), minus 1 -- a uniform in [0, 1)
+SPAI_PHX float sample_u01_f32(uint64_t seed, uint64_t game_id, uint64_t move_no) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t ctr[4] = {(uint32_t)move_no, (uint32_t)(move_no >> 32), (uint32_t)game_id, (uint32_t)(game_id >> 32)};
+    uint32_t out[4];
+    philox4x32(ctr, key, out);
+    return __builtin_bit_cast(float, (out[0] >> 9) | 0x3F800000u) - 1.0f;
 }
 
-template <class Pow>
-inline int weighted_index_with(const float *visits, int n, float temperature, double u, Pow &&pw) {
-    double cum[512];
-    double total = 0.0;
+// WeightedIndex::<f32>::new(w) then sample (rand 0.8, learner_concurrent.rs:192-193):
+// the running f32 total before each later weight, Uniform::new(0, total) shrinking
+// its scale one ulp at a time while scale * (1 - 2^-23) >= total, chosen = u01 *
+// scale + 0, and the index = the number of running totals <= chosen (so a zero
+// weight is never picked).  -1: no item, an invalid (negative / NaN) weight or an
+// infinite total (the reference panics); -2: all weights zero (panics too)
+SPAI_PHX int weighted_index_f32(const float *w, int n, float u01) {
+    if (n <= 0) return -1;
+    float total = 0.0f;
+    for (int i = 0; i < n; ++i) {
+        if (!(w[i] >= 0.0f)) return -1;
+        total = i ? total + w[i] : w[i];
+    }
+    if (total == 0.0f) return -2;
+    if (!(total <= 3.40282347e38f)) return -1;
+    const float max_rand = 1.0f - 1.1920929e-7f;
+    float scale = total;
+    while (scale * max_rand >= total) scale = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, scale) - 1u);
+    const float chosen = u01 * scale + 0.0f;
+    int idx = 0;
+    float run = 0.0f;
+    for (int i = 0; i + 1 < n; ++i) {
+        run = i ? run + w[i] : w[i];
+        if (run <= chosen) idx = i + 1;
+    }
+    return idx;
+}
+
+// the move draw of SelfPlayWorker::self_play over child visit counts: weights
+// (visit_count as f32).powf(temperature), host powf (glibc, as Rust's f32::powf)
+inline int weighted_index(const float *visits, int n, float temperature, float u01) {
+    float w[512];
     if (n <= 0 || n > 512) return -1;
-    for (int i = 0; i < n; ++i) {
-        total += pw(visits[i], temperature);
-        cum[i] = total;
-    }
-    return weighted_index_cum(cum, n, total, u);
-}
-
-inline int weighted_index(const float *visits, int n, float temperature, double u) {
-    return weighted_index_with(visits, n, temperature, u,
-                               [](float v, float t) { return std::pow((double)v, (double)t); });
+    for (int i = 0; i < n; ++i) w[i] = ::powf(visits[i], temperature);
+    return weighted_index_f32(w, n, u01);
 }
 
 }  // namespace spai

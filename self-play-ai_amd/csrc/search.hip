@@ -454,8 +454,8 @@ __global__ void k_root_stats(TreeView T, const uint32_t *__restrict__ active, ui
 
 // Self-play's move after a search call (learner_concurrent.rs:177-203), per active
 // tree: the root's visit counts, the sampled child (the Philox uniform of philox.h
-// and WeightedIndex over visits^T, the weights from the host's std::pow table, so
-// the pick is the host sampler's bit for bit), and for a game that goes on the
+// and rand's WeightedIndex<f32> over (visits as f32).powf(T), the weights from a
+// table of the host's powf, so the pick is the host sampler's bit for bit), and for a game that goes on the
 // child written as the tree's new root (use_subtree).  One record per tree goes
 // back to the host: [0] the root's children word, [1..7] the child visit counts,
 // [8] the pick (index | action << 8 | new status << 16; without one, bit 31 and
@@ -474,7 +474,7 @@ struct ChainCounts {
     const uint32_t *p[spai_engine::kChains];
 };
 __global__ void k_advance(TreeView T, RootsOut R, const uint32_t *__restrict__ active, uint32_t n_active,
-                          const double *__restrict__ pow_tab, uint32_t pow_n, uint64_t seed, uint64_t gid_base,
+                          const float *__restrict__ pow_tab, uint32_t pow_n, uint64_t seed, uint64_t gid_base,
                           uint64_t move_no, const uint32_t *err, ChainCounts cc, int nchain, uint32_t n_counts,
                           uint32_t *out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -502,14 +502,13 @@ __global__ void k_advance(TreeView T, RootsOut R, const uint32_t *__restrict__ a
     rec[9] = T.evals[t];
     bool beyond = false;
     int idx = -1;   // weighted_index_with: -1 without children
-    if (nch > 0) {
-        double cum[c4::kActions], total = 0.0;
+    if (nch > 0) {   // WeightedIndex<f32> over (visits as f32).powf(T) (learner_concurrent.rs:189-193)
+        float w[c4::kActions];
         for (uint32_t k = 0; k < nch; ++k) {
             beyond |= vis[k] >= pow_n;
-            total += pow_tab[min(vis[k], pow_n - 1)];
-            cum[k] = total;
+            w[k] = pow_tab[min(vis[k], pow_n - 1)];
         }
-        idx = weighted_index_cum(cum, (int)nch, total, sample_uniform(seed, gid_base + t, move_no));
+        idx = weighted_index_f32(w, (int)nch, sample_u01_f32(seed, gid_base + t, move_no));
     }
     if (beyond || idx < 0) {
         rec[8] = kPickNone | (beyond ? kPickNoTable : (uint32_t)(-idx));
@@ -1023,17 +1022,17 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
     // every game's history in flat per-game slabs of the longest game (42 plies):
     // growing 3 x n_games vectors made every game reallocate at the same moves
     constexpr size_t kPlies = c4::kCells;
-    // visits^T for every count a root child can reach (a search call adds at most
-    // ns visits to a root, a game has at most kPlies moves), by the std::pow the
-    // host sampler used, once per temperature
+    // (visits as f32).powf(T) for every count a root child can reach (a search call
+    // adds at most ns visits to a root, a game has at most kPlies moves), by the
+    // host's powf (the f32::powf of the reference), once per temperature
     const uint32_t pow_n = ns * (uint32_t)kPlies + 1;
-    const double temp = (double)e->cfg.temperature;
+    const float temp = e->cfg.temperature;
     if (e->pow_tab_t != temp || e->pow_tab.n < pow_n) {
-        std::vector<double> tab(pow_n);
-        for (uint32_t k = 0; k < pow_n; ++k) tab[k] = std::pow((double)k, temp);
-        e->pow_tab_t = -1.0;
+        std::vector<float> tab(pow_n);
+        for (uint32_t k = 0; k < pow_n; ++k) tab[k] = ::powf((float)k, temp);   // Rust f32::powf = libm powf
+        e->pow_tab_t = -1.0f;
         SPAI_TRY(e->pow_tab.alloc(pow_n));
-        SPAI_HIP(hipMemcpy(e->pow_tab.p, tab.data(), pow_n * sizeof(double), hipMemcpyHostToDevice));
+        SPAI_HIP(hipMemcpy(e->pow_tab.p, tab.data(), pow_n * sizeof(float), hipMemcpyHostToDevice));
         e->pow_tab_t = temp;
     }
     // records, then every chain's leaf counters (tail mode: up to ns + kTailChunk + 1)

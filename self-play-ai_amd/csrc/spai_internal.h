@@ -212,8 +212,8 @@ struct spai_engine {
     // self-play's move step on the device (search.hip k_advance): visits^T for every
     // visit count a game can reach (the host's std::pow), and the per-move records,
     // read back into one of two pinned buffers (move m's is read while m + 1 runs)
-    spai::DevBuf<double> pow_tab;
-    double pow_tab_t = -1.0;
+    spai::DevBuf<float> pow_tab;       // (visit count as f32).powf(T), host glibc powf
+    float pow_tab_t = -1.0f;
     spai::DevBuf<uint32_t> move_out;
     uint32_t *h_move[2] = {nullptr, nullptr};
     size_t h_move_n = 0;

@@ -963,7 +963,7 @@ int spai_ttt_selfplay_run(spai_ttt *e, uint32_t n_games, uint64_t gid_base, spai
             Rec r;
             r.s = roots[t];
             visit_policy(roots[t], s, r.pol, nullptr, vis);
-            const double u = sample_uniform(e->cfg.seed, gid_base + t, move_no);
+            const float u = sample_u01_f32(e->cfg.seed, gid_base + t, move_no);
             const int idx = weighted_index(vis, (int)s[0], e->cfg.temperature, u);
             SPAI_CHECK(idx >= 0, SPAI_ERR_NAN, "WeightedIndex over all-zero visits (the reference panics)");
             pick[k] = (uint32_t)idx;

@@ -20,6 +20,8 @@ Outputs (all small):
   mcts_hash.json                  root visits after K sims, self-play streams
   net_c4_2x64.npz, net_ttt_2x64.npz  params, inputs, logits, values, priors
 """
+import ctypes
+import ctypes.util
 import json
 import math
 import os
@@ -250,26 +252,40 @@ def philox4x32(ctr, key):
     return c0, c1, c2, c3
 
 
-def uniform(seed, game_id, move_no):
+def u01_f32(seed, game_id, move_no):
+    """rand 0.8's UniformFloat<f32> draw: the top 23 bits of the first Philox word
+    as a float in [1, 2), minus 1"""
     o = philox4x32((move_no & M32, move_no >> 32, game_id & M32, game_id >> 32), (seed & M32, seed >> 32))
-    bits = (((o[0] << 21) ^ (o[1] >> 11))) & ((1 << 53) - 1)
-    return bits / 9007199254740992.0
+    one_two = struct.unpack("<f", struct.pack("<I", (o[0] >> 9) | 0x3F800000))[0]
+    return f32(one_two - 1.0)
 
 
-def weighted_index(visits, temperature, u):
-    cum = []
-    total = 0.0
-    for v in visits:
-        total += math.pow(float(v), float(f32(temperature)))
+_LIBM = ctypes.CDLL(ctypes.util.find_library("m"))
+_LIBM.powf.restype = ctypes.c_float
+_LIBM.powf.argtypes = [ctypes.c_float, ctypes.c_float]
+
+
+def powf(x, y):
+    """f32::powf (Rust calls the C library's powf)"""
+    return float(_LIBM.powf(x, y))
+
+
+def weighted_index(visits, temperature, u01):
+    """WeightedIndex::<f32>::new(visits.powf(T)).sample (rand 0.8,
+    learner_concurrent.rs:189-193): f32 running totals, Uniform::new(0, total)
+    shrinking its scale one ulp at a time while scale * (1 - 2^-23) >= total,
+    chosen = u01 * scale, index = #running totals <= chosen"""
+    w = [f32(powf(f32(v), f32(temperature))) for v in visits]
+    cum, total = [], w[0]
+    for x in w[1:]:
         cum.append(total)
-    x = u * total
-    last = 0   # never a zero-weight item (rand's WeightedIndex)
-    for i, cv in enumerate(cum):
-        if cv > x:
-            return i
-        if cv > (cum[i - 1] if i else 0.0):
-            last = i
-    return last
+        total = f32(total + x)
+    max_rand = f32(1.0 - 1.1920929e-7)
+    scale = total
+    while f32(scale * max_rand) >= total:
+        scale = struct.unpack("<f", struct.pack("<I", struct.unpack("<I", struct.pack("<f", scale))[0] - 1))[0]
+    chosen = f32(f32(u01 * scale) + 0.0)
+    return sum(1 for c in cum if c <= chosen)
 
 
 def splitmix64(x):
@@ -408,7 +424,7 @@ def self_play(game_cls, n_games, num_searches, temperature=1.25, seed=7, c=2.0):
             g = active[k]
             t = trees[g]
             pol, kids = res[k]
-            idx = weighted_index([n for (_, _, n) in kids], temperature, uniform(seed, g, move_no))
+            idx = weighted_index([n for (_, _, n) in kids], temperature, u01_f32(seed, g, move_no))
             sel = kids[idx][0]
             hist[g][0].append(t.arena[0].state)
             hist[g][1].append(pol)
@@ -686,7 +702,13 @@ def main():
         json.dump(rules, f, separators=(",", ":"))
     with open(os.path.join(HERE, "rules_ttt.json"), "w") as f:
         json.dump({"traces": rules_traces(TTT, 300, 3)}, f, separators=(",", ":"))
+    mcts_main()
+    np.savez_compressed(os.path.join(HERE, "net_c4_2x64.npz"), **net_golden("c4", 2, 64, 1234, 256, 5))
+    np.savez_compressed(os.path.join(HERE, "net_ttt_2x64.npz"), **net_golden("ttt", 2, 64, 99, 64, 6))
+    learner_main()
 
+
+def mcts_main():
     mcts = {"search": [], "selfplay": {}}
     rng = random.Random(11)
     for case in range(12):
@@ -715,10 +737,6 @@ def main():
     with open(os.path.join(HERE, "mcts_hash.json"), "w") as f:
         json.dump(mcts, f, separators=(",", ":"))
 
-    np.savez_compressed(os.path.join(HERE, "net_c4_2x64.npz"), **net_golden("c4", 2, 64, 1234, 256, 5))
-    np.savez_compressed(os.path.join(HERE, "net_ttt_2x64.npz"), **net_golden("ttt", 2, 64, 99, 64, 6))
-    learner_main()
-
 
 def learner_main():
     np.savez_compressed(os.path.join(HERE, "learner_c4_1x64.npz"), **learner_golden())
@@ -728,5 +746,7 @@ if __name__ == "__main__":
     # `gen_golden.py learner` regenerates only the training fixture
     if len(sys.argv) > 1 and sys.argv[1] == "learner":
         learner_main()
+    elif len(sys.argv) > 1 and sys.argv[1] == "mcts":   # `gen_golden.py mcts`: only mcts_hash.json
+        mcts_main()
     else:
         main()

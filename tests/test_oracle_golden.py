@@ -122,10 +122,17 @@ def test_sampler_matches_python(oracle):
     spec.loader.exec_module(gg)
     L = oracle.lib()
     for seed, gid, mv in [(0, 0, 0), (7, 3, 11), (2**40 + 5, 123456, 2**33 + 1)]:
-        assert L.or_uniform(seed, gid, mv) == gg.uniform(seed, gid, mv)
+        u = L.or_u01_f32(seed, gid, mv)
+        assert u == gg.u01_f32(seed, gid, mv) and 0.0 <= u < 1.0
     vis = np.array([3, 0, 10, 1, 7], np.float32)
-    for u in [0.0, 0.1, 0.5, 0.77, 0.999999]:
+    for u in [0.0, 0.1, 0.5, 0.77, 0.99999994]:
         assert L.or_weighted_index(oracle._f(vis), 5, np.float32(1.25), u) == gg.weighted_index(vis, 1.25, u)
+    # a zero-weight child is never drawn, whatever the uniform (rand's WeightedIndex)
+    rng = np.random.default_rng(0)
+    for _ in range(2000):
+        u = float(np.float32(rng.random()))
+        i = L.or_weighted_index(oracle._f(vis), 5, np.float32(1.25), u)
+        assert vis[i] > 0 and i == gg.weighted_index(vis, 1.25, u)
 
 
 def test_mcts_search_hash(oracle):
