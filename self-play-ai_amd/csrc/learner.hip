@@ -807,24 +807,41 @@ __global__ __launch_bounds__(kBn) void k_bn_bwd(const float *__restrict__ da, co
 // one workgroup per sample: policy logits (1344 -> 7), value (126 -> 1, tanh),
 // loss terms and the output gradients
 //   dlogits = (softmax * sum(pi) - pi) / B,  dpre = 2 (v - z) / B * (1 - v^2)
+// FUSED: rp / rv are the head convs' z, and their BatchNorm + ReLU (train mode,
+// k_bn_fwd's arithmetic) is applied here from the convs' partials (BnIn), writing
+// the activations a for the backward
+template <bool FUSED>
 __global__ __launch_bounds__(kThreads) void k_heads_loss(const float *__restrict__ rp, const float *__restrict__ rv,
                                                          const float *__restrict__ wp, const float *__restrict__ bp,
                                                          const float *__restrict__ wv, const float *__restrict__ bv,
                                                          const float *__restrict__ pi, const float *__restrict__ zv,
                                                          int B, float *__restrict__ dlogits, float *__restrict__ dpre,
-                                                         float *__restrict__ loss_terms) {
+                                                         float *__restrict__ loss_terms, BnIn bnp, BnIn bnv) {
     __shared__ float part[kThreads / 64][8];
+    __shared__ float stp[FUSED ? kBnStatFloats : 1], stv[FUSED ? kBnStatFloats : 1];
     const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const float *xp = rp + (size_t)b * 32 * kCells, *xv = rv + (size_t)b * 3 * kCells;
+    if constexpr (FUSED) {
+        bn_in_stats(bnp, 32, stp);
+        bn_in_stats(bnv, 3, stv);
+        __syncthreads();
+    }
+    auto act = [&](float z, const float *st, int c, float *a_out, int k) {
+        if constexpr (!FUSED) return z;
+        const float y = fmaxf(st[128 + c] * ((z - st[c]) * st[64 + c]) + st[192 + c], 0.f);
+        a_out[k] = y;
+        return y;
+    };
     // one pass over the features: 7 policy logits and the value pre-activation at
     // once; wave sums by shuffles, then the 4 wave partials in order
     float acc8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int k = threadIdx.x; k < 32 * kCells; k += kThreads) {
-        const float xk = xp[k];
+        const float xk = act(xp[k], stp, k / kCells, bnp.a_out + (size_t)b * 32 * kCells, k);
 #pragma unroll
         for (int o = 0; o < 7; ++o) acc8[o] += xk * wp[o * 32 * kCells + k];
     }
-    for (int k = threadIdx.x; k < 3 * kCells; k += kThreads) acc8[7] += xv[k] * wv[k];
+    for (int k = threadIdx.x; k < 3 * kCells; k += kThreads)
+        acc8[7] += act(xv[k], stv, k / kCells, bnv.a_out + (size_t)b * 3 * kCells, k) * wv[k];
 #pragma unroll
     for (int o = 0; o < 8; ++o) {
 #pragma unroll
@@ -972,7 +989,7 @@ int learner_alloc_batch(spai_learner *L, uint32_t B) {
     }
     SPAI_TRY(L->d0.alloc(act));
     SPAI_TRY(L->d1.alloc(act));
-    SPAI_TRY(L->bn_part.alloc((size_t)(2 * L->blocks + 1) * L->hidden * B * 2));
+    SPAI_TRY(L->bn_part.alloc((size_t)(2 * L->blocks + 3) * L->hidden * B * 2));   // trunk + the two heads
     SPAI_TRY(L->d2.alloc(act));
     if (L->blocks > 0) SPAI_TRY(L->dzb.alloc((size_t)2 * L->blocks * B * L->hidden * kCells));
     SPAI_TRY(L->dlogits.alloc((size_t)B * 7));
@@ -1046,6 +1063,7 @@ int launch_conv(const float *in, int cin, const float *wk, const float *bias, in
     SPAI_CONV_CASE(4, kGradStats)
     SPAI_CONV_CASE(32, 0)
     SPAI_CONV_CASE(64, 0)
+    SPAI_CONV_CASE(64, kStatsOut)
     SPAI_CONV_CASE(64, kBnIn)
     SPAI_CONV_CASE(64, kBnIn | kStatsOut)
     SPAI_CONV_CASE(64, kBnGrad)
@@ -1273,8 +1291,9 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
         // layer l's BN input to its consumer: the residual is the block input a[l - 2] for a block's second conv
         auto bn_of = [&](int l) {
             const spai_learner::Conv &c = L->convs[l];
-            return BnIn{part_of(l), P + c.g, P + c.be, (l >= 2 && l % 2 == 0) ? L->a[l - 2].p : nullptr, L->a[l].p,
-                        L->mean[l].p, L->invstd[l].p, P + c.mu, P + c.var, (int)B, eps, mom};
+            const bool res = l >= 2 && l <= last && l % 2 == 0;
+            return BnIn{part_of(l), P + c.g, P + c.be, res ? L->a[l - 2].p : nullptr, L->a[l].p, L->mean[l].p,
+                        L->invstd[l].p, P + c.mu, P + c.var, (int)B, eps, mom};
         };
         {
             const spai_learner::Conv &c = L->convs[0];
@@ -1288,18 +1307,18 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
         if (crc == SPAI_OK) {   // the policy head conv applies the trunk's last BN and writes the trunk output
             const spai_learner::Conv &c = L->convs[pol];
             const BnIn b = bn_of(last);
-            crc = launch_conv(L->z[last].p, c.ci, W + c.wk, P + c.b, c.co, L->z[pol].p, (int)B, false, st, &b, nullptr);
+            crc = launch_conv(L->z[last].p, c.ci, W + c.wk, P + c.b, c.co, L->z[pol].p, (int)B, false, st, &b,
+                              part_of(pol));
         }
         h = L->a[last].p;
         if (crc == SPAI_OK) {
             const spai_learner::Conv &c = L->convs[val];
-            crc = launch_conv(h, c.ci, W + c.wk, P + c.b, c.co, L->z[val].p, (int)B, false, st);
+            crc = launch_conv(h, c.ci, W + c.wk, P + c.b, c.co, L->z[val].p, (int)B, false, st, nullptr, part_of(val));
         }
-        for (int l : {pol, val}) {
-            const spai_learner::Conv &c = L->convs[l];
-            k_bn_fwd<<<c.co, kBn, 0, st>>>(L->z[l].p, c.co, (int)B, eps, mom, L->mean[l].p, L->invstd[l].p, P + c.mu,
-                                           P + c.var, P + c.g, P + c.be, nullptr, L->a[l].p);
-        }
+        // the heads' BN + ReLU inside the loss kernel
+        k_heads_loss<true><<<B, kThreads, 0, st>>>(L->z[pol].p, L->z[val].p, P + L->pol_w, P + L->pol_b, P + L->val_w,
+                                                   P + L->val_b, pi_in, z_in, (int)B, L->dlogits.p, L->dpre.p,
+                                                   L->loss_terms.p, bn_of(pol), bn_of(val));
     } else {
         conv_bn_act(0, x_in, nullptr);
         h = L->a[0].p;
@@ -1311,9 +1330,10 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
         conv_bn_act(pol, h, nullptr);
         conv_bn_act(val, h, nullptr);
     }
-    k_heads_loss<<<B, kThreads, 0, st>>>(L->a[pol].p, L->a[val].p, P + L->pol_w, P + L->pol_b, P + L->val_w,
-                                         P + L->val_b, pi_in, z_in, (int)B, L->dlogits.p, L->dpre.p,
-                                         L->loss_terms.p);
+    if (!fuse)
+        k_heads_loss<false><<<B, kThreads, 0, st>>>(L->a[pol].p, L->a[val].p, P + L->pol_w, P + L->pol_b, P + L->val_w,
+                                                    P + L->val_b, pi_in, z_in, (int)B, L->dlogits.p, L->dpre.p,
+                                                    L->loss_terms.p, BnIn{}, BnIn{});
 
     // ---------------- backward
     // heads: linears -> relu/BN -> conv; dh (d0) = dgrad(policy) + dgrad(value)
