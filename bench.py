@@ -79,6 +79,9 @@ def parse():
     ap.add_argument("--sims", type=int, default=800, help="MCTS simulations per move")
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--stream", action="store_true",
+                    help="play the steps' games as one stream through G tree slots (spai_selfplay_stream: a slot "
+                         "takes the next game when its game ends) instead of one lockstep batch of G per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-games", type=int, default=100,
                     help="games the CPU baseline plays to completion inside this run: the reference worker's batch "
@@ -354,8 +357,19 @@ def main():
         _, st = eng.self_play(G, game_id_base=base, collect=False)
         return st
 
-    for i in range(args.warmup):
-        step(-1 - i)
+    def stream(first, k):
+        """k steps' worth of games through G tree slots; rank r plays ids
+        [(first * world + r * k) * G, + k * G) (world 1: the lockstep steps' ids)"""
+        base = (first * dist.world + dist.rank * k) * G
+        _, st = eng.self_play(k * G, game_id_base=base, collect=False, window=G)
+        return st
+
+    if args.stream:
+        if args.warmup:
+            stream(-args.warmup, args.warmup)
+    else:
+        for i in range(args.warmup):
+            step(-1 - i)
     eng.sync()
     dist.barrier()
     # HIP events on every 32nd search iteration of each chain: ~0.6 % overhead (every
@@ -363,10 +377,15 @@ def main():
     eng.set_timing(not args.no_timing, stride=32)
     tot = dict(sims=0.0, games=0.0, evals=0.0, positions=0.0, moves=0.0)
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        st = step(i)
+    if args.stream:
+        st = stream(0, args.steps)
         for k in tot:
             tot[k] += st[k]
+    else:
+        for i in range(args.steps):
+            st = step(i)
+            for k in tot:
+                tot[k] += st[k]
     eng.sync()
     dist.barrier()
     dt = time.perf_counter() - t0
@@ -414,8 +433,10 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic: self-play from the empty board, random-init net (tch default init, seed %d)" % args.seed,
-        "config": {"workload": "Connect4 self-play, %d games/GPU x %d sims/move, %dx64 ResNet bf16, to completion"
-                               % (G, args.sims, args.blocks),
+        "config": {"workload": "Connect4 self-play, %d games/GPU x %d sims/move, %dx64 ResNet bf16, to completion%s"
+                               % (G, args.sims, args.blocks,
+                                  (", %d games streamed through %d tree slots" % (G * args.steps, G))
+                                  if args.stream else ""),
                    "model": "c4-resnet-%dx64" % args.blocks, "games_per_gpu": G, "sims_per_move": args.sims,
                    "global_batch": G * dist.world, "parallelism": "dp%d (games sharded, no collective)" % dist.world},
         "work": {"sims": sims, "games": games, "evals": evals, "positions": positions},   # summed over ranks

@@ -193,6 +193,17 @@ typedef struct spai_selfplay_stats {
 } spai_selfplay_stats;
 int spai_selfplay_run(spai_engine *eng, uint32_t n_games, uint64_t game_id_base, spai_sample_sink sink, void *user,
                       spai_selfplay_stats *stats);
+/* The same n_games games (ids game_id_base + i, i < n_games; every game's moves,
+ * samples and outcome identical to spai_selfplay_run's, the draws keyed by the
+ * game id and the game's own move number) played through `window` tree slots:
+ * a finished game's slot takes the next game at once, so the device keeps
+ * `window` games in flight until the last ones finish instead of searching
+ * ever fewer trees as a lockstep batch runs out (the reference's main.rs:169-186
+ * keeps the device busy with 6 concurrent workers instead).  The sink sees
+ * finished games in the order they finish.  window >= n_games is
+ * spai_selfplay_run; window <= max_trees. */
+int spai_selfplay_stream(spai_engine *eng, uint32_t n_games, uint32_t window, uint64_t game_id_base,
+                         spai_sample_sink sink, void *user, spai_selfplay_stats *stats);
 
 /* ------------------------------------------------------------------ profiling
  * Per-kernel average device time of the last spai_selfplay_run / spai_search

@@ -354,6 +354,20 @@ int spai_selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_
     return selfplay_run(e, n_games, gid_base, sink, user, stats);
 }
 
+int spai_selfplay_stream(spai_engine *e, uint32_t n_games, uint32_t window, uint64_t gid_base, spai_sample_sink sink,
+                         void *user, spai_selfplay_stats *stats) {
+    ENG_CHECK(e);
+    if (e->game != SPAI_GAME_CONNECT4) {
+        set_error("self-play streaming: Connect4 engines");
+        return SPAI_ERR_UNSUPPORTED;
+    }
+    if (window == 0) {
+        set_error("window must be > 0");
+        return SPAI_ERR_INVALID;
+    }
+    return selfplay_run(e, n_games, gid_base, sink, user, stats, window);
+}
+
 int spai_engine_set_timing(spai_engine *e, int enabled) {
     ENG_CHECK(e);
     KernelTimer &K = e->timer;

@@ -474,9 +474,9 @@ struct ChainCounts {
     const uint32_t *p[spai_engine::kChains];
 };
 __global__ void k_advance(TreeView T, RootsOut R, const uint32_t *__restrict__ active, uint32_t n_active,
-                          const float *__restrict__ pow_tab, uint32_t pow_n, uint64_t seed, uint64_t gid_base,
-                          uint64_t move_no, const uint32_t *err, ChainCounts cc, int nchain, uint32_t n_counts,
-                          uint32_t *out) {
+                          const float *__restrict__ pow_tab, uint32_t pow_n, uint64_t seed,
+                          const uint64_t *__restrict__ slot_gid, uint32_t *__restrict__ slot_move,
+                          const uint32_t *err, ChainCounts cc, int nchain, uint32_t n_counts, uint32_t *out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) {
@@ -508,7 +508,7 @@ __global__ void k_advance(TreeView T, RootsOut R, const uint32_t *__restrict__ a
             beyond |= vis[k] >= pow_n;
             w[k] = pow_tab[min(vis[k], pow_n - 1)];
         }
-        idx = weighted_index_f32(w, (int)nch, sample_u01_f32(seed, gid_base + t, move_no));
+        idx = weighted_index_f32(w, (int)nch, sample_u01_f32(seed, slot_gid[t], slot_move[t]));
     }
     if (beyond || idx < 0) {
         rec[8] = kPickNone | (beyond ? kPickNoTable : (uint32_t)(-idx));
@@ -519,6 +519,7 @@ __global__ void k_advance(TreeView T, RootsOut R, const uint32_t *__restrict__ a
     c4::State cs = rs;
     (void)c4::next_state(rs, a, cs);
     rec[8] = (uint32_t)idx | (uint32_t)a << 8 | (uint32_t)cs.status << 16;
+    slot_move[t] += 1;   // the game's next move number (its sampling counter)
     if (cs.status == c4::kOngoing) {
         R.root[t] = first + (uint32_t)idx;
         R.x[t] = cs.x;
@@ -527,6 +528,26 @@ __global__ void k_advance(TreeView T, RootsOut R, const uint32_t *__restrict__ a
         R.status[t] = cs.status;
     }
 }
+// self-play: tree slot list[i] starts game list[n + i] (refill) or game gid_base +
+// slot (list == null, every slot in [0, n)): an empty board as its root, an empty
+// arena, move number 0
+__global__ void k_slots_start(TreeView T, RootsOut R, uint64_t *__restrict__ slot_gid,
+                              uint32_t *__restrict__ slot_move, const uint32_t *__restrict__ list, uint32_t n,
+                              uint64_t gid_base) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t t = list ? list[i] : i;
+    T.nodes[(size_t)t * T.cap] = make_uint4(0u, 0u, 0u, kNoChildren);
+    T.next_free[t] = 1;
+    R.root[t] = 0;
+    R.x[t] = 0;
+    R.o[t] = 0;
+    R.n[t] = 0;
+    R.status[t] = c4::kOngoing;
+    slot_gid[t] = gid_base + (list ? list[n + i] : i);
+    slot_move[t] = 0;
+}
+
 __global__ void k_trees_init(TreeView T, uint32_t first_tree, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -689,6 +710,9 @@ int trees_create(spai_engine *e, uint32_t n) {
         SPAI_TRY(T.slot.alloc(n));
         SPAI_TRY(T.left.alloc(n));
         SPAI_TRY(T.evals.alloc(n + 1));   // [n]: the search call's max over trees (k_root_stats)
+        SPAI_TRY(T.slot_gid.alloc(n));
+        SPAI_TRY(T.slot_move.alloc(n));
+        SPAI_TRY(T.refill.alloc(2 * (size_t)n));
         SPAI_TRY(e->active.alloc(n));
         SPAI_TRY(e->stats.alloc((size_t)n * 8));
         for (Batch &B : e->batch) {   // one double-buffered leaf batch per search chain
@@ -1010,10 +1034,15 @@ int tree_size(spai_engine *e, uint32_t t, uint32_t *nodes) {
 // launched as soon as the host knows which games go on; this move's bookkeeping
 // (policy targets, histories, finished games to the sink, in the reference's
 // order) runs on the host while it searches.
+// window < n_games (spai_selfplay_stream): the games run through `window` tree
+// slots; a slot whose game ended takes the next game before the next search call.
+// Each game's draws are keyed by its id and its own move number (per slot on the
+// device), so every game is the one spai_selfplay_run would play.
 int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sample_sink sink, void *user,
-                 spai_selfplay_stats *stats) {
+                 spai_selfplay_stats *stats, uint32_t window) {
     const auto t_start = std::chrono::steady_clock::now();
-    SPAI_TRY(trees_create(e, n_games));
+    const uint32_t W = (window == 0 || window >= n_games) ? n_games : window;   // tree slots
+    SPAI_TRY(trees_create(e, W));
     SPAI_CHECK(e->cfg.eval != SPAI_EVAL_NET || e->net, SPAI_ERR_INVALID,
                "eval = NET but no net set (spai_engine_set_net)");
     Trees &T = e->trees;
@@ -1036,7 +1065,7 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
         e->pow_tab_t = temp;
     }
     // records, then every chain's leaf counters (tail mode: up to ns + kTailChunk + 1)
-    const size_t n_words = 2 + (size_t)n_games * kMoveRec +
+    const size_t n_words = 2 + (size_t)W * kMoveRec +
                            (size_t)spai_engine::kChains * (std::max(ns, 1u) + kTailChunk + 1);
     if (e->h_move_n < n_words) {
         e->h_move_n = 0;
@@ -1050,13 +1079,17 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
         SPAI_TRY(e->move_out.alloc(n_words));
         e->h_move_n = n_words;
     }
-    std::vector<c4::State> h_states((size_t)n_games * kPlies);
-    std::vector<float> h_pol((size_t)n_games * kPlies * 7);
-    std::vector<int32_t> h_moves((size_t)n_games * kPlies);
-    std::vector<uint32_t> h_len(n_games, 0);
+    std::vector<c4::State> h_states((size_t)W * kPlies);   // per tree slot
+    std::vector<float> h_pol((size_t)W * kPlies * 7);
+    std::vector<int32_t> h_moves((size_t)W * kPlies);
+    std::vector<uint32_t> h_len(W, 0);
     std::vector<uint32_t> act[2];   // this move's trees and the next move's (the launch reads them)
-    act[0].resize(n_games);
-    for (uint32_t i = 0; i < n_games; ++i) act[0][i] = i;
+    act[0].resize(W);
+    for (uint32_t i = 0; i < W; ++i) act[0][i] = i;
+    std::vector<uint32_t> slot_game(W);   // the game (index < n_games) each slot plays
+    for (uint32_t i = 0; i < W; ++i) slot_game[i] = i;
+    uint32_t next_game = W;
+    std::vector<uint32_t> refill[2];   // per move parity: [slots..., games...] uploaded for k_slots_start
     std::vector<float> enc, sv;
     double sims = 0, evals = 0, games = 0, positions = 0, moves = 0;
     // optional per-move trace (diagnostics): SPAI_TRACE_MOVES=<csv path>
@@ -1071,15 +1104,25 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
     const TreeView tv = tree_view(e);
     const RootsOut ro{T.root.p, T.root_x.p, T.root_o.p, T.root_n.p, T.root_status.p};
     SearchRun R;
-    // enqueue move mv over the trees a: the search call, k_advance, the records' copy to dst
-    auto launch = [&](const std::vector<uint32_t> &a, uint64_t mv, uint32_t *dst) -> int {
+    // every slot starts its first game (id gid_base + slot) at move 0
+    k_slots_start<<<(W + 255) / 256, 256, 0, st>>>(tv, ro, T.slot_gid.p, T.slot_move.p, nullptr, W, gid_base);
+    SPAI_HIP(hipGetLastError());
+    // enqueue a move over the trees a: slots in rf start their new games, the search
+    // call, k_advance, the records' copy to dst
+    auto launch = [&](const std::vector<uint32_t> &a, const std::vector<uint32_t> &rf, uint32_t *dst) -> int {
         const uint32_t na = (uint32_t)a.size();
+        if (!rf.empty()) {
+            const uint32_t nr = (uint32_t)(rf.size() / 2);
+            SPAI_HIP(hipMemcpyAsync(T.refill.p, rf.data(), rf.size() * 4, hipMemcpyHostToDevice, st));
+            k_slots_start<<<(nr + 255) / 256, 256, 0, st>>>(tv, ro, T.slot_gid.p, T.slot_move.p, T.refill.p, nr,
+                                                           gid_base);
+        }
         SPAI_TRY(search_launch(e, na, a.data(), ns, R));
         ChainCounts cc{};
         for (int h = 0; h < R.nchain; ++h) cc.p[h] = e->batch[h].iter_counts.p;
         k_advance<<<(na + 63) / 64, 64, 0, st>>>(tv, ro, e->active.p, na, e->pow_tab.p, (uint32_t)e->pow_tab.n,
-                                                 e->cfg.seed, gid_base, mv, e->err.p, cc, R.nchain, R.n_counts,
-                                                 e->move_out.p);
+                                                 e->cfg.seed, T.slot_gid.p, T.slot_move.p, e->err.p, cc, R.nchain,
+                                                 R.n_counts, e->move_out.p);
         SPAI_HIP(hipGetLastError());
         const size_t words = 2 + (size_t)na * kMoveRec + (size_t)R.nchain * R.n_counts;
         SPAI_HIP(hipMemcpyAsync(dst, e->move_out.p, words * 4, hipMemcpyDeviceToHost, st));
@@ -1099,7 +1142,7 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
     uint64_t move_no = 0;
     int cur = 0;
     auto tm0 = std::chrono::steady_clock::now();
-    SPAI_TRY(launch(act[0], 0, e->h_move[0]));
+    SPAI_TRY(launch(act[0], refill[0], e->h_move[0]));
     while (!act[cur].empty()) {
         const std::vector<uint32_t> &A = act[cur];
         const uint32_t na = (uint32_t)A.size();
@@ -1119,15 +1162,32 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
         sims += (double)na * ns;
         evals += ev;
         moves += 1;
-        // the games that go on, in order (trees_vec.remove keeps it), and their next move
+        // the games that go on, in order (trees_vec.remove keeps it), and their next move;
+        // streaming: slots whose game ended take the next games (appended)
         std::vector<uint32_t> &N = act[cur ^ 1];
+        std::vector<uint32_t> &RF = refill[(move_no + 1) & 1];
         N.clear();
+        RF.clear();
         auto tm2 = tm1;
         if (!stop) {
             for (uint32_t i = 0; i < na; ++i)
                 if (((mo[2 + (size_t)i * kMoveRec + 8] >> 16) & 0xFFu) == c4::kOngoing) N.push_back(A[i]);
+            for (uint32_t i = 0; i < na && next_game < n_games; ++i)
+                if (((mo[2 + (size_t)i * kMoveRec + 8] >> 16) & 0xFFu) != c4::kOngoing) {
+                    RF.push_back(A[i]);
+                    RF.push_back(next_game++);
+                }
+            const size_t nr = RF.size() / 2;
+            if (nr) {   // [slots..., games...]
+                std::vector<uint32_t> tmp(RF);
+                for (size_t j = 0; j < nr; ++j) {
+                    RF[j] = tmp[2 * j];
+                    RF[nr + j] = tmp[2 * j + 1];
+                    N.push_back(RF[j]);
+                }
+            }
             tm2 = std::chrono::steady_clock::now();
-            if (!N.empty()) SPAI_TRY(launch(N, move_no + 1, e->h_move[(move_no + 1) & 1]));
+            if (!N.empty()) SPAI_TRY(launch(N, RF, e->h_move[(move_no + 1) & 1]));
         }
         const auto tm3 = std::chrono::steady_clock::now();
         for (int k = (int)na - 1; k >= 0; --k) {   // for i in (0..trees_vec.len()).rev()
@@ -1177,13 +1237,26 @@ int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sampl
                     // x.get_current_player() == state.get_current_player() ? value : -value
                     sv[j] = ((s.n & 1) == (cs.n & 1)) ? v : -v;
                 }
-                if (sink) sink(user, (uint32_t)(gid_base + t), (uint32_t)m, enc.data(), hp, sv.data(), hm);
+                if (sink) sink(user, (uint32_t)(gid_base + slot_game[t]), (uint32_t)m, enc.data(), hp, sv.data(), hm);
                 games += 1;
                 positions += (double)m;
                 h_len[t] = 0;
             } else {                                          // use_subtree(selected_id), already on the device
                 T.h_root[t] = first + (uint32_t)idx;
                 T.h_root_state[t] = cs;
+                T.h_root_nch[t] = 0;
+            }
+        }
+        {   // streaming: the refilled slots' host mirrors start their new games (k_slots_start
+            // reset the device side ahead of the search call already in flight)
+            const std::vector<uint32_t> &RFc = refill[(move_no + 1) & 1];
+            const size_t nr = RFc.size() / 2;
+            for (size_t j = 0; j < nr; ++j) {
+                const uint32_t t = RFc[j];
+                slot_game[t] = RFc[nr + j];
+                T.h_root[t] = 0;
+                T.h_root_state[t] = c4::State{0, 0, 0, c4::kOngoing};
+                T.h_root_first[t] = 0;
                 T.h_root_nch[t] = 0;
             }
         }

@@ -84,6 +84,9 @@ struct Trees {
     DevBuf<uint32_t> slot;          // [n_trees] leaf slot in the current batch (select -> expand)
     DevBuf<uint32_t> left;          // [n_trees] search iterations left (tail run-on mode, search.hip)
     DevBuf<uint32_t> evals;         // [n_trees] live leaves of the current search call (tail-mode policy)
+    DevBuf<uint64_t> slot_gid;      // [n_trees] self-play: the game id a tree slot plays (its sampling stream)
+    DevBuf<uint32_t> slot_move;     // [n_trees] self-play: that game's move number (k_advance advances it)
+    DevBuf<uint32_t> refill;        // [2 n_trees] self-play streaming: slots taking a new game, and the games
     // host mirrors of the root bookkeeping
     std::vector<uint32_t> h_root;
     std::vector<c4::State> h_root_state;
@@ -297,7 +300,7 @@ int tree_use_subtree(spai_engine *e, uint32_t t, uint32_t child);
 int tree_node(spai_engine *e, uint32_t t, uint32_t node, spai_c4_state *st, uint32_t *visits, float *w);
 int tree_size(spai_engine *e, uint32_t t, uint32_t *nodes);
 int selfplay_run(spai_engine *e, uint32_t n_games, uint64_t gid_base, spai_sample_sink sink, void *user,
-                 spai_selfplay_stats *stats);
+                 spai_selfplay_stats *stats, uint32_t window = 0);
 
 inline c4::State from_abi(const spai_c4_state &s) { return c4::State{s.x, s.o, s.num_actions_played, s.status}; }
 inline spai_c4_state to_abi(const c4::State &s) {

@@ -32,7 +32,7 @@ SYMBOLS = [
     "spai_mask_invalid", "spai_rules_bench", "spai_net_num_params", "spai_net_init_params", "spai_net_create",
     "spai_net_destroy", "spai_net_forward", "spai_predict", "spai_engine_set_net", "spai_trees_create",
     "spai_tree_reset", "spai_search", "spai_tree_use_subtree", "spai_tree_node", "spai_tree_size",
-    "spai_selfplay_run", "spai_engine_set_timing", "spai_engine_timing", "spai_engine_timing_items",
+    "spai_selfplay_run", "spai_selfplay_stream", "spai_engine_set_timing", "spai_engine_timing", "spai_engine_timing_items",
     "spai_net_phase_cycles", "spai_net_bench", "spai_net_bench_conc", "spai_adam_config_default", "spai_learner_create", "spai_learner_destroy",
     "spai_learner_train_batch", "spai_learner_params", "spai_learner_grads", "spai_learner_activation", "spai_comm_unique_id",
     "spai_learner_set_comm", "spai_learner_broadcast", "spai_learner_set_host_comm", "spai_learner_last_batch",
@@ -162,6 +162,7 @@ def lib():
         L.spai_tree_node.argtypes = [vp, u32, u32, vp, vp, vp]
         L.spai_tree_size.argtypes = [vp, u32, vp]
         L.spai_selfplay_run.argtypes = [vp, u32, u64, SINK, vp, P(SelfPlayStats)]
+        L.spai_selfplay_stream.argtypes = [vp, u32, u32, u64, SINK, vp, P(SelfPlayStats)]
         L.spai_engine_set_timing.argtypes = [vp, i32]
         L.spai_engine_timing.argtypes = [vp, vp, vp]
         L.spai_engine_timing_items.argtypes = [vp, vp, vp]
@@ -407,7 +408,10 @@ class Engine:
         return n.value
 
     # ---- self-play
-    def self_play(self, n_games, game_id_base=0, collect=True):
+    def self_play(self, n_games, game_id_base=0, collect=True, window=None):
+        """SelfPlayWorker::self_play over n_games games (spai_selfplay_run); window:
+        play them through that many tree slots, refilled as games end
+        (spai_selfplay_stream)"""
         games = []
 
         def sink(user, gid, n, enc, pol, val, moves):
@@ -420,7 +424,10 @@ class Engine:
 
         cb = SINK(sink)
         st = SelfPlayStats()
-        _check(lib().spai_selfplay_run(self.h, n_games, game_id_base, cb, None, C.byref(st)))
+        if window is None:
+            _check(lib().spai_selfplay_run(self.h, n_games, game_id_base, cb, None, C.byref(st)))
+        else:
+            _check(lib().spai_selfplay_stream(self.h, n_games, window, game_id_base, cb, None, C.byref(st)))
         return games, {k: getattr(st, k) for k, _ in SelfPlayStats._fields_}
 
     # ---- profiling

@@ -790,3 +790,35 @@ def test_learner_bn_fusion_matches_unfused(spai, tmp_path):
     d = np.abs(p1 - p0)
     assert d.max() <= 2 * steps * 1e-3, d.max()
     assert np.median(d) <= 1e-5, np.median(d)   # the bulk of the parameters moves alike
+
+
+@pytest.mark.parametrize("window", [37, 64, 160])
+def test_self_play_stream_matches_oracle_per_game(spai, oracle, window):
+    """spai_selfplay_stream: 160 games through `window` tree slots, a slot taking
+    the next game as soon as its game ends (each game's draws keyed by its id and
+    its own move number).  Every game -- its positions, visit policies, signed
+    values and moves -- must be the oracle's lockstep self-play of the same game
+    id bit for bit; only the order in which games finish differs.  window = 160
+    is spai_selfplay_run itself, emission order included"""
+    n, sims, seed, base = 160, 24, 5, 300
+    e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_HASH, seed=seed)
+    games, stats = e.self_play(n, game_id_base=base, window=window)
+    e.close()
+    ref = oracle.self_play(oracle.GAME_CONNECT4, n, sims, seed, eval_kind=oracle.EVAL_HASH, max_plies=42,
+                           game_id_base=base)
+    by_game = {}
+    k = 0
+    while k < len(ref["value"]):
+        g = int(ref["game"][k])
+        m = int(np.sum(ref["game"] == g))
+        by_game[g + base] = (ref["enc"][k:k + m], ref["policy"][k:k + m], ref["value"][k:k + m])
+        k += m
+    assert sorted(g["game"] for g in games) == sorted(by_game) and len(games) == n
+    for g in games:
+        enc, pol, val = by_game[g["game"]]
+        np.testing.assert_array_equal(g["enc"], enc)
+        np.testing.assert_array_equal(g["policy"], pol)
+        np.testing.assert_array_equal(g["value"], val)
+    assert stats["games"] == n and stats["sims"] == ref["sims"]
+    if window == n:   # lockstep: the reference's emission order as well
+        assert [g["game"] for g in games] == [int(v) + base for v in dict.fromkeys(ref["game"].tolist())]
