@@ -9,3 +9,10 @@ rc=$?; grep -E "passed|failed" $O/pytest_gpu.log | tail -2; [ $rc -eq 0 ] || { g
 SKIP_TESTS=1 bash scripts/gpu_r05_c.sh && SKIP_TESTS=1 bash scripts/gpu_r05_d.sh
 timeout -k 10 300 python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-isolated --no-rules-bench --no-chess > $O/bench_stdout.txt 2> $O/bench_stderr.txt; rc=$?
 echo "bench rc=$rc stdout lines: $(wc -l < $O/bench_stdout.txt)"; head -c 300 $O/bench_stdout.txt; echo
+for r in 1 2; do
+  for v in "" "--stream"; do
+    n=lock; [ -n "$v" ] && n=stream
+    timeout -k 10 300 python3 bench.py --steps ${SSTEPS:-4} --warmup 1 --no-cpu-baseline --no-isolated --no-rules-bench --no-chess $v > $O/bench_${n}_$r.json 2> $O/bench_${n}_$r.err || { tail -5 $O/bench_${n}_$r.err; exit 1; }
+    python3 -c "import json; d=json.loads([l for l in open('$O/bench_${n}_$r.json') if l.startswith('{')][-1]); print('$n $r', round(d['value']/1e6,3), 'M sims/s', round(d['games_per_sec'],1), 'games/s', round(d['roofline']['frac'],4))"
+  done
+done
