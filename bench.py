@@ -79,9 +79,13 @@ def parse():
     ap.add_argument("--sims", type=int, default=800, help="MCTS simulations per move")
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--stream", action="store_true",
-                    help="play the steps' games as one stream through G tree slots (spai_selfplay_stream: a slot "
-                         "takes the next game when its game ends) instead of one lockstep batch of G per step")
+    ap.add_argument("--lockstep", action="store_true",
+                    help="one lockstep batch of G games per step (every game starts together; the batch thins out "
+                         "as games end) instead of the default stream: the steps' K x G games played through G tree "
+                         "slots, a slot taking the next game when its game ends (spai_selfplay_stream)")
+    ap.add_argument("--stream", action="store_true", help=argparse.SUPPRESS)   # the default; kept for old scripts
+    ap.add_argument("--no-lockstep-ref", action="store_true",
+                    help="skip the one-step lockstep figure reported beside the streamed headline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-games", type=int, default=100,
                     help="games the CPU baseline plays to completion inside this run: the reference worker's batch "
@@ -364,7 +368,8 @@ def main():
         _, st = eng.self_play(k * G, game_id_base=base, collect=False, window=G)
         return st
 
-    if args.stream:
+    streaming = not args.lockstep
+    if streaming:
         if args.warmup:
             stream(-args.warmup, args.warmup)
     else:
@@ -377,7 +382,7 @@ def main():
     eng.set_timing(not args.no_timing, stride=32)
     tot = dict(sims=0.0, games=0.0, evals=0.0, positions=0.0, moves=0.0)
     t0 = time.perf_counter()
-    if args.stream:
+    if streaming:
         st = stream(0, args.steps)
         for k in tot:
             tot[k] += st[k]
@@ -436,7 +441,7 @@ def main():
         "config": {"workload": "Connect4 self-play, %d games/GPU x %d sims/move, %dx64 ResNet bf16, to completion%s"
                                % (G, args.sims, args.blocks,
                                   (", %d games streamed through %d tree slots" % (G * args.steps, G))
-                                  if args.stream else ""),
+                                  if streaming else ", one lockstep batch per step"),
                    "model": "c4-resnet-%dx64" % args.blocks, "games_per_gpu": G, "sims_per_move": args.sims,
                    "global_batch": G * dist.world, "parallelism": "dp%d (games sharded, no collective)" % dist.world},
         "work": {"sims": sims, "games": games, "evals": evals, "positions": positions},   # summed over ranks
@@ -466,6 +471,19 @@ def main():
                                     "avg_launch_ms": ev["avg_ms"], "launches_sampled": ev["launches"],
                                     "note": "shared CUs: launches x avg_launch_ms exceeds the step time"}},
     }
+    # the lockstep schedule beside the streamed headline: one step of G games started
+    # together (game ids after the timed region's), rank 0 of a 1-rank run
+    if streaming and dist.rank == 0 and dist.world == 1 and not args.no_lockstep_ref:
+        eng.set_timing(False)
+        eng.sync()
+        t1 = time.perf_counter()
+        ls = step(args.steps)
+        eng.sync()
+        d1 = time.perf_counter() - t1
+        result["lockstep"] = {"value": ls["sims"] / d1, "games_per_sec": ls["games"] / d1, "ms_per_step": d1 * 1e3,
+                              "frac": ls["evals"] / d1 * fpe / 1e12 / BF16_PEAK_TFLOPS, "steps": 1,
+                              "note": "one batch of %d games started together and played to completion "
+                                      "(the reference worker's schedule; bench.py --lockstep times K of these)" % G}
     # the same forward launch ALONE on the GPU (spai_net_bench, HIP events, random reachable
     # positions) at the timed region's mean leaves per launch, at one chain's (x2) and at the
     # full-batch sizes: the isolated-kernel roofline beside the shared-CU per-launch figure above

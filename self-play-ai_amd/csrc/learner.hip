@@ -35,6 +35,8 @@ constexpr int kCells = 42, kRows = 6, kCols = 7;
 constexpr int kPad = 72;          // (6+2) x (7+2) zero-padded plane
 constexpr int kPlane = 73;        // its LDS stride (odd, so channels spread over the banks)
 constexpr int kThreads = 256;
+constexpr int kTickDbias = 8;     // BatchNorm hand-off counters: tick[0..7] channel slices, tick[8] the bias-gradient merge
+constexpr int kTicks = 16;
 
 // ------------------------------------------------------------------ conv 3x3 on f32 MFMA
 // Every conv of the step is a GEMM on v_mfma_f32_16x16x4_f32 (exact f32: an
@@ -141,7 +143,10 @@ __device__ __forceinline__ void stage_planes_fast(const float *__restrict__ xb, 
 // step (blockIdx.y = entry of the table built at learner_create):
 //   desc[8 y ..] = {param offset, cin, cout, cinp, coutp, dgrad, packed offset, 0}
 constexpr int kPackDesc = 8;
-__global__ void k_pack_all(const float *__restrict__ P, const uint32_t *__restrict__ desc, float *__restrict__ wall) {
+// (it also zeroes the BatchNorm hand-off counters ahead of the step's convs)
+__global__ void k_pack_all(const float *__restrict__ P, const uint32_t *__restrict__ desc, float *__restrict__ wall,
+                           unsigned *__restrict__ tick) {
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < kTicks) tick[threadIdx.x] = 0u;
     const uint32_t *d = desc + kPackDesc * blockIdx.y;
     const int cin = (int)d[1], cout = (int)d[2], cinp = (int)d[3], coutp = (int)d[4];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -155,73 +160,140 @@ __global__ void k_pack_all(const float *__restrict__ P, const uint32_t *__restri
 }
 
 // BatchNorm (train mode) of a conv's input, applied while the consumer conv
-// stages it (MODE & kBnIn): the producer conv left per-(channel, sample)
-// partials {sum, centred sum of squares} over the 42 cells (MODE & kStatsOut);
-// every consumer workgroup merges the B partials of each input channel in the
-// same fixed order (Chan's pairwise variance: N var = sum_b Q_b + 42 sum_b
-// (m_b - mean)^2), so all of them hold the same mean / invstd, and stages
-// a = relu(gamma (z - mean) invstd + beta [+ res]).  The slice-0 workgroups of
-// each sample write a (the backward's mask and weight-gradient input), the first
-// workgroup the batch statistics and the running statistics (momentum, unbiased
-// variance) -- what k_bn_fwd did in a kernel of its own.
+// stages it (MODE & kBnIn).  The producer conv (MODE & kStatsOut) leaves
+// per-(channel, sample) partials {sum, centred sum of squares} over the 42 cells,
+// and the last of its workgroups to finish a channel slice merges that slice's B
+// partials in a fixed order (Chan's pairwise variance: N var = sum_b Q_b + 42
+// sum_b (m_b - mean)^2) into the batch mean / invstd and the running statistics
+// (momentum, unbiased variance) -- what k_bn_fwd did in a kernel of its own.  The
+// consumer stages a = relu(gamma (z - mean) invstd + beta [+ res]) from those
+// 4 x 64 floats; its slice-0 workgroups write a (the backward's mask and
+// weight-gradient input).
+//
+// The hand-off inside the producer launch (cdna_hip_programming.md §6 Guideline
+// 16, counter form): every partial is stored write-through (sc1), each storing
+// wave drains, the workgroup barrier, then one lane's agent-scope ticket add; the
+// workgroup that draws the slice's last ticket reads the partials with sc1 loads
+// and resets the counter.  The merge order is fixed, so the result does not
+// depend on which workgroup finishes last.
 constexpr int kBnIn = 1, kStatsOut = 2, kBnGrad = 4, kGradStats = 8;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
 struct BnIn {
-    const float2 *part;           // [cin][B] producer partials
+    float2 *part;                 // [c][B] producer partials (kStatsOut)
     const float *gamma, *beta;
     const float *res;             // residual (block input) [B][cin][42], or null
     float *a_out;                 // activations [B][cin][42]
     float *mean, *invstd, *run_mean, *run_var;
     int B;
     float eps, momentum;
+    unsigned *tick;               // the producer's slice counters
 };
 constexpr int kBnStatFloats = 5 * 64;   // LDS: per input channel 4 (forward) or 5 (backward) statistics
+constexpr int kLdsFlags = 4;            // LDS: the ticket results
+
+__device__ __forceinline__ void store_part(float2 *p, float x, float y) {   // write-through (sc1)
+    const unsigned long long u = ((unsigned long long)__float_as_uint(y) << 32) | __float_as_uint(x);
+    __hip_atomic_store((gu64 *)p, u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float2 load_part(const float2 *p) {   // sc1: no stale L1 copy
+    const unsigned long long u = __hip_atomic_load((gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_float2(__uint_as_float((unsigned)u), __uint_as_float((unsigned)(u >> 32)));
+}
+__device__ __forceinline__ void store_part1(float *p, float x) {
+    __hip_atomic_store((gu32 *)p, __float_as_uint(x), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float load_part1(const float *p) {
+    return __uint_as_float(__hip_atomic_load((gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+// sum over the tpc consecutive lanes of a channel (butterfly: the same value on each)
+__device__ __forceinline__ float chan_sum(float v, int tpc) {
+    for (int o = 1; o < tpc; o <<= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// the merge of channels [c0, c0 + ch) of a forward producer (ch = 16 or 64: 16 or
+// 4 lanes per channel, samples strided over them)
+__device__ __forceinline__ void fin_bn_fwd(const BnIn &bo, int c0, int ch, int cout) {
+    const int tpc = kThreads / ch, c = c0 + threadIdx.x / tpc, q = threadIdx.x % tpc, B = bo.B;
+    const bool ok = c < cout;
+    const float2 *pp = bo.part + (size_t)c * B;
+    float s = 0.f;
+    if (ok)
+        for (int b = q; b < B; b += tpc) s += load_part(pp + b).x;
+    s = chan_sum(s, tpc);
+    const int n = B * kCells;
+    const float mu = s / (float)n;
+    float q2 = 0.f;
+    if (ok)
+        for (int b = q; b < B; b += tpc) {
+            const float2 v = load_part(pp + b);
+            const float d = v.x / (float)kCells - mu;
+            q2 += v.y + (float)kCells * (d * d);
+        }
+    q2 = chan_sum(q2, tpc);
+    if (q == 0 && ok) {
+        const float var = q2 / (float)n;
+        bo.mean[c] = mu;
+        bo.invstd[c] = 1.0f / sqrtf(var + bo.eps);
+        bo.run_mean[c] = (1.0f - bo.momentum) * bo.run_mean[c] + bo.momentum * mu;
+        bo.run_var[c] = (1.0f - bo.momentum) * bo.run_var[c] +
+                        bo.momentum * (n > 1 ? var * (float)n / (float)(n - 1) : var);
+    }
+}
 
 // The backward of a = relu(bn(z) [+ res]) fused the same way (kBnGrad): the
 // producer of da (the data gradient of the layer above, kGradStats) leaves per
 // (channel, sample) partials {sum dy, sum dy xhat} with dy = da [a > 0] and
-// xhat = (z - mean) invstd; the consumer (this layer's data-gradient conv)
-// merges them into dbeta = sum dy and dgamma = sum dy xhat and stages
-// dz = gamma invstd / N (N dy - dbeta - xhat dgamma) (k_bn_bwd's arithmetic),
-// writing dz for the weight gradient and dy for the residual's skip path from
-// its slice-0 workgroups.  The conv bias gradient (sum dz) comes from the weight
-// gradient (a column of ones, k_wgrad_mfma BIAS).
+// xhat = (z - mean) invstd, and its slice's last workgroup merges them into
+// dbeta = sum dy and dgamma = sum dy xhat; the consumer (this layer's
+// data-gradient conv) stages dz = gamma invstd / N (N dy - dbeta - xhat dgamma)
+// (k_bn_bwd's arithmetic), writing dz for the weight gradient and dy for the
+// residual's skip path from its slice-0 workgroups.  Those also leave per-sample
+// sums of dz, merged by their last workgroup into the conv bias gradient.
 struct BnGrad {
-    const float2 *part;           // [c][B] {sum dy, sum dy xhat} of this layer
     const float *a, *z, *mean, *invstd, *gamma;
+    const float *dgamma, *dbeta;  // merged by the producer of da
     float *dz_out, *dy_out;       // [B][c][42] (dy_out may be null)
-    float *dgamma, *dbeta;
+    float *db_part, *dbias;       // [c][B] per-sample dz sums; the conv bias gradient
+    unsigned *tick;
     int B;
 };
 struct GradStats {                // the partials for the layer whose da this conv produces
     const float *a, *z, *mean, *invstd;
     float2 *part;                 // [c][B]
+    float *dgamma, *dbeta;        // that layer's merged gradients
+    unsigned *tick;
 };
 
-__device__ __forceinline__ void bn_grad_stats(const BnGrad &bg, int cin, float *st) {
-    const int c = threadIdx.x >> 2, qq = threadIdx.x & 3, B = bg.B;
-    const float2 *pp = bg.part + (size_t)c * B;
+__device__ __forceinline__ void fin_bn_grad(const GradStats &gs, int c0, int ch, int cout, int B) {
+    const int tpc = kThreads / ch, c = c0 + threadIdx.x / tpc, q = threadIdx.x % tpc;
+    const bool ok = c < cout;
+    const float2 *pp = gs.part + (size_t)c * B;
     float s1 = 0.f, s2 = 0.f;
-    if (c < cin)
-        for (int b = qq; b < B; b += 4) {
-            const float2 v = pp[b];
+    if (ok)
+        for (int b = q; b < B; b += tpc) {
+            const float2 v = load_part(pp + b);
             s1 += v.x;
             s2 += v.y;
         }
-    s1 += __shfl_xor(s1, 1, 64);
-    s1 += __shfl_xor(s1, 2, 64);
-    s2 += __shfl_xor(s2, 1, 64);
-    s2 += __shfl_xor(s2, 2, 64);
-    if (qq == 0 && c < cin) {
+    s1 = chan_sum(s1, tpc);
+    s2 = chan_sum(s2, tpc);
+    if (q == 0 && ok) {
+        gs.dbeta[c] = s1;
+        gs.dgamma[c] = s2;
+    }
+}
+
+__device__ __forceinline__ void bn_grad_stats(const BnGrad &bg, int cin, float *st) {
+    const int c = threadIdx.x;
+    if (c < cin) {
         const float is = bg.invstd[c];
-        st[c] = s1;
-        st[64 + c] = s2;
+        st[c] = bg.dbeta[c];
+        st[64 + c] = bg.dgamma[c];
         st[128 + c] = bg.mean[c];
         st[192 + c] = is;
-        st[256 + c] = bg.gamma[c] * is / (float)(B * kCells);
-        if (blockIdx.x == 0 && blockIdx.y == 0) {
-            bg.dbeta[c] = s1;
-            bg.dgamma[c] = s2;
-        }
+        st[256 + c] = bg.gamma[c] * is / (float)(bg.B * kCells);
     }
 }
 
@@ -273,40 +345,14 @@ __device__ __forceinline__ void stage_planes_dz(const float *__restrict__ dab, i
     }
 }
 
-// per-channel statistics of the input from the producer's partials -> LDS st[4][64]
+// per-channel statistics of the input (merged by its producer) -> LDS st[4][64]
 __device__ __forceinline__ void bn_in_stats(const BnIn &bn, int cin, float *st) {
-    const int c = threadIdx.x >> 2, qq = threadIdx.x & 3, B = bn.B;
-    const float2 *pp = bn.part + (size_t)c * B;
-    float s = 0.f;
-    if (c < cin)
-        for (int b = qq; b < B; b += 4) s += pp[b].x;
-    s += __shfl_xor(s, 1, 64);   // the 4 quarters in a fixed order, the same value on all 4 lanes
-    s += __shfl_xor(s, 2, 64);
-    const int n = B * kCells;
-    const float mu = s / (float)n;
-    float q = 0.f;
-    if (c < cin)
-        for (int b = qq; b < B; b += 4) {
-            const float2 v = pp[b];
-            const float d = v.x / (float)kCells - mu;
-            q += v.y + (float)kCells * (d * d);
-        }
-    q += __shfl_xor(q, 1, 64);
-    q += __shfl_xor(q, 2, 64);
-    const float var = q / (float)n;
-    const float is = 1.0f / sqrtf(var + bn.eps);
-    if (qq == 0 && c < cin) {
-        st[c] = mu;
-        st[64 + c] = is;
+    const int c = threadIdx.x;
+    if (c < cin) {
+        st[c] = bn.mean[c];
+        st[64 + c] = bn.invstd[c];
         st[128 + c] = bn.gamma[c];
         st[192 + c] = bn.beta[c];
-        if (blockIdx.x == 0 && blockIdx.y == 0) {
-            bn.mean[c] = mu;
-            bn.invstd[c] = is;
-            bn.run_mean[c] = (1.0f - bn.momentum) * bn.run_mean[c] + bn.momentum * mu;
-            bn.run_var[c] = (1.0f - bn.momentum) * bn.run_var[c] +
-                            bn.momentum * (n > 1 ? var * (float)n / (float)(n - 1) : var);
-        }
     }
 }
 
@@ -361,8 +407,7 @@ template <int CINP, int NT, int MODE = 0, int MTS = 3>
 __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict__ in, int cin,
                                                         const float *__restrict__ wk, const float *__restrict__ bias,
                                                         int cout, int coutp_all, float *__restrict__ out,
-                                                        int accumulate, BnIn bn, float2 *__restrict__ stats_out,
-                                                        int stats_b, BnGrad bg, GradStats gs) {
+                                                        int accumulate, BnIn bn, BnIn bo, BnGrad bg, GradStats gs) {
     constexpr int KS = 4 / NT, CSN = CINP / 4, KSTEPS = 9 * CSN, PER = KSTEPS / KS;
     static_assert(4 % NT == 0 && KSTEPS % KS == 0, "4 waves: NT channel tiles x KS whole K parts");
     extern __shared__ float sm[];
@@ -442,7 +487,7 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
                 for (int r = 0; r < 4; ++r) dst[mt * 64 * 4 + r] = acc[mt][r];
         }
         __syncthreads();
-        if (part > 0) return;
+        if (part == 0)
 #pragma unroll
         for (int q = 1; q < KS; ++q) {
             const float *src = red + (((q - 1) * 3) * 64 + lane) * 4 + nt * (3 * 3 * 64 * 4);
@@ -453,67 +498,127 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
         }
     }
     const int n = co0 + nt * 16 + row;   // D[row = 4 kq + r][col = lane & 15]: col = channel, row = position
-    if (n >= cout) return;
-    const float bv = bias ? bias[n] : 0.f;
-    float *ob = out + ((size_t)b * cout + n) * kCells;
-    float fin[MTS][4];   // the stored values (kGradStats)
-#pragma unroll
-    for (int mt = 0; mt < MTS; ++mt)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int p = (mt0 + mt) * 16 + 4 * kq + r;
-            fin[mt][r] = 0.f;
-            if (p < kCells) {
-                const float v = acc[mt][r] + bv;
-                fin[mt][r] = accumulate ? ob[p] + v : v;
-                ob[p] = fin[mt][r];
-            }
-        }
-    if constexpr ((MODE & kGradStats) != 0) {   // the next BN backward's partials of channel n, sample b
-        static_assert(MTS == 3, "statistics need the whole board");
-        const size_t base = ((size_t)b * cout + n) * kCells;
-        const float mu = gs.mean[n], is = gs.invstd[n];
-        float s1 = 0.f, s2 = 0.f;
+    // the waves that hold a finished tile (part 0); no early return: every wave
+    // reaches the hand-off's barriers below
+    const bool live = (KS == 1 || part == 0) && n < cout;
+    const int b0 = (int)gridDim.x;   // the partials' row length: the batch
+    if (live) {
+        const float bv = bias ? bias[n] : 0.f;
+        float *ob = out + ((size_t)b * cout + n) * kCells;
+        float fin[MTS][4];   // the stored values (kGradStats)
 #pragma unroll
         for (int mt = 0; mt < MTS; ++mt)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int p = (mt0 + mt) * 16 + 4 * kq + r;
+                fin[mt][r] = 0.f;
                 if (p < kCells) {
-                    const float d = gs.a[base + p] > 0.f ? fin[mt][r] : 0.f;
-                    s1 += d;
-                    s2 += d * ((gs.z[base + p] - mu) * is);
+                    const float v = acc[mt][r] + bv;
+                    fin[mt][r] = accumulate ? ob[p] + v : v;
+                    ob[p] = fin[mt][r];
                 }
             }
-        s1 += __shfl_xor(s1, 16, 64);
-        s1 += __shfl_xor(s1, 32, 64);
-        s2 += __shfl_xor(s2, 16, 64);
-        s2 += __shfl_xor(s2, 32, 64);
-        if (kq == 0) gs.part[(size_t)n * stats_b + b] = make_float2(s1, s2);
-    }
-    if constexpr ((MODE & kStatsOut) != 0) {   // the consumer's BN partials of channel n, sample b
-        static_assert(MTS == 3, "statistics need the whole board");
-        float s = 0.f;
+        if constexpr ((MODE & kGradStats) != 0) {   // the next BN backward's partials of channel n, sample b
+            static_assert(MTS == 3, "statistics need the whole board");
+            const size_t base = ((size_t)b * cout + n) * kCells;
+            const float mu = gs.mean[n], is = gs.invstd[n];
+            float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int mt = 0; mt < MTS; ++mt)
+            for (int mt = 0; mt < MTS; ++mt)
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if ((mt0 + mt) * 16 + 4 * kq + r < kCells) s += acc[mt][r] + bv;
-        s += __shfl_xor(s, 16, 64);   // the 4 lanes of the channel, a fixed order, the same value on each
-        s += __shfl_xor(s, 32, 64);
-        const float m = s / (float)kCells;
-        float q = 0.f;
-#pragma unroll
-        for (int mt = 0; mt < MTS; ++mt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if ((mt0 + mt) * 16 + 4 * kq + r < kCells) {
-                    const float d = (acc[mt][r] + bv) - m;
-                    q += d * d;
+                for (int r = 0; r < 4; ++r) {
+                    const int p = (mt0 + mt) * 16 + 4 * kq + r;
+                    if (p < kCells) {
+                        const float d = gs.a[base + p] > 0.f ? fin[mt][r] : 0.f;
+                        s1 += d;
+                        s2 += d * ((gs.z[base + p] - mu) * is);
+                    }
                 }
-        q += __shfl_xor(q, 16, 64);
-        q += __shfl_xor(q, 32, 64);
-        if (kq == 0) stats_out[(size_t)n * stats_b + b] = make_float2(s, q);
+            s1 += __shfl_xor(s1, 16, 64);
+            s1 += __shfl_xor(s1, 32, 64);
+            s2 += __shfl_xor(s2, 16, 64);
+            s2 += __shfl_xor(s2, 32, 64);
+            if (kq == 0) store_part(gs.part + (size_t)n * b0 + b, s1, s2);
+        }
+        if constexpr ((MODE & kStatsOut) != 0) {   // the consumer's BN partials of channel n, sample b
+            static_assert(MTS == 3, "statistics need the whole board");
+            float s = 0.f;
+#pragma unroll
+            for (int mt = 0; mt < MTS; ++mt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if ((mt0 + mt) * 16 + 4 * kq + r < kCells) s += acc[mt][r] + bv;
+            s += __shfl_xor(s, 16, 64);   // the 4 lanes of the channel, a fixed order, the same value on each
+            s += __shfl_xor(s, 32, 64);
+            const float m = s / (float)kCells;
+            float q = 0.f;
+#pragma unroll
+            for (int mt = 0; mt < MTS; ++mt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if ((mt0 + mt) * 16 + 4 * kq + r < kCells) {
+                        const float d = (acc[mt][r] + bv) - m;
+                        q += d * d;
+                    }
+            q += __shfl_xor(q, 16, 64);
+            q += __shfl_xor(q, 32, 64);
+            if (kq == 0) store_part(bo.part + (size_t)n * b0 + b, s, q);
+        }
+    }
+    constexpr bool kStats = (MODE & (kStatsOut | kGradStats)) != 0, kDb = (MODE & kBnGrad) != 0;
+    if constexpr (kStats || kDb) {
+        static_assert(MTS == 3, "the hand-off counts whole-board workgroups");
+        // kBnGrad: the slice-0 workgroups' per-sample bias-gradient partials, sum_p dz
+        // over the staged planes (4 lanes per channel, a fixed order)
+        const bool dbw = kDb && blockIdx.y == 0;
+        if (dbw) {
+            const int c = threadIdx.x >> 2, q = threadIdx.x & 3;
+            float s = 0.f;
+            if (c < cin)
+                for (int p = q; p < kCells; p += 4) s += xs[c * kPlane + (p / kCols + 1) * 9 + p % kCols + 1];
+            s = chan_sum(s, 4);
+            if (q == 0 && c < cin) store_part1(bg.db_part + (size_t)c * b0 + b, s);
+        }
+        float *flag = sm + CINP * kPlane + 2 * 2304 + kBnStatFloats;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its sc1 stores
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned *tick = kStats ? ((MODE & kStatsOut) ? bo.tick : gs.tick) : nullptr;
+            float l1 = 0.f, l2 = 0.f;
+            if (kStats) {
+                const unsigned t = __hip_atomic_fetch_add((gu32 *)(tick + blockIdx.y), 1u, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                if (t == gridDim.x - 1) {
+                    l1 = 1.f;
+                    __hip_atomic_store((gu32 *)(tick + blockIdx.y), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            if (dbw) {
+                const unsigned t = __hip_atomic_fetch_add((gu32 *)(bg.tick + kTickDbias), 1u, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT);
+                if (t == gridDim.x - 1) {
+                    l2 = 1.f;
+                    __hip_atomic_store((gu32 *)(bg.tick + kTickDbias), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            flag[0] = l1;
+            flag[1] = l2;
+        }
+        __syncthreads();
+        // the last arrival merges (sc1 loads: no acquire needed, Guideline 16)
+        if (kStats && flag[0] != 0.f) {
+            const int ch = 16 * NT, c0 = MTS == 3 ? 16 * NT * (int)blockIdx.y : 0;
+            if constexpr ((MODE & kStatsOut) != 0) fin_bn_fwd(bo, c0, ch, cout);
+            if constexpr ((MODE & kGradStats) != 0) fin_bn_grad(gs, c0, ch, cout, b0);
+        }
+        if (kDb && flag[1] != 0.f) {   // the conv bias gradient: 4 lanes per channel, a fixed order
+            const int c = threadIdx.x >> 2, q = threadIdx.x & 3;
+            float s = 0.f;
+            if (c < cin)
+                for (int bb = q; bb < b0; bb += 4) s += load_part1(bg.db_part + (size_t)c * b0 + bb);
+            s = chan_sum(s, 4);
+            if (q == 0 && c < cin) bg.dbias[c] = s;
+        }
     }
 }
 
@@ -989,7 +1094,8 @@ int learner_alloc_batch(spai_learner *L, uint32_t B) {
     }
     SPAI_TRY(L->d0.alloc(act));
     SPAI_TRY(L->d1.alloc(act));
-    SPAI_TRY(L->bn_part.alloc((size_t)(2 * L->blocks + 3) * L->hidden * B * 2));   // trunk + the two heads
+    // trunk + the two heads' partials, the bias-gradient partials [64][B], the hand-off counters
+    SPAI_TRY(L->bn_part.alloc((size_t)(2 * L->blocks + 3) * L->hidden * B * 2 + (size_t)L->hidden * B + kTicks));
     SPAI_TRY(L->d2.alloc(act));
     if (L->blocks > 0) SPAI_TRY(L->dzb.alloc((size_t)2 * L->blocks * B * L->hidden * kCells));
     SPAI_TRY(L->dlogits.alloc((size_t)B * 7));
@@ -1011,25 +1117,25 @@ int learner_alloc_batch(spai_learner *L, uint32_t B) {
 // k-steps) keeps one workgroup per sample with a wave per channel tile.
 template <int CINP, int MODE>
 int launch_conv_t(int B, size_t lds, hipStream_t st, const float *in, int cin, const float *wk, const float *bias,
-                  int cout, float *out, int acc, const BnIn &bn, float2 *stats, const BnGrad &bg, const GradStats &gs) {
+                  int cout, float *out, int acc, const BnIn &bn, const BnIn &bo, const BnGrad &bg, const GradStats &gs) {
     constexpr int ks = 9 * CINP / 4;
     const int nt = round16(cout) / 16;
 #ifdef SPAI_SLICE_NT2   // variant: 32-channel slices, the K split over 2 wave pairs
     if constexpr (ks % 2 == 0) {
         if (nt % 2 == 0) {
             k_conv_mfma<CINP, 2, MODE><<<dim3(B, nt / 2), kThreads, lds, st>>>(in, cin, wk, bias, cout, 16 * nt, out,
-                                                                              acc, bn, stats, B, bg, gs);
+                                                                              acc, bn, bo, bg, gs);
             return SPAI_OK;
         }
     }
 #endif
     if constexpr (ks % 4 == 0) {
         k_conv_mfma<CINP, 1, MODE><<<dim3(B, nt), kThreads, lds, st>>>(in, cin, wk, bias, cout, 16 * nt, out, acc, bn,
-                                                                      stats, B, bg, gs);
+                                                                      bo, bg, gs);
         return SPAI_OK;
     }
     if (nt == 4) {
-        k_conv_mfma<CINP, 4, MODE><<<dim3(B), kThreads, lds, st>>>(in, cin, wk, bias, cout, 64, out, acc, bn, stats, B,
+        k_conv_mfma<CINP, 4, MODE><<<dim3(B), kThreads, lds, st>>>(in, cin, wk, bias, cout, 64, out, acc, bn, bo,
                                                                   bg, gs);
         return SPAI_OK;
     }
@@ -1038,25 +1144,32 @@ int launch_conv_t(int B, size_t lds, hipStream_t st, const float *in, int cin, c
 }
 
 // bn: the input's BatchNorm applied while staging (in = the producer's z), or
-// null; stats: this conv's per-(channel, sample) BN partials for its consumer, or
-// null; bg: the input (= da) turned into this layer's dz while staging (the BN
-// backward), or null; gs: the BN-backward partials of the layer whose da this
-// conv writes, or null
+// null; bo: this conv's BatchNorm, whose per-(channel, sample) partials it leaves
+// and merges (kStatsOut), or null; bg: the input (= da) turned into this layer's
+// dz while staging (the BN backward), or null; gs: the BN-backward partials of the
+// layer whose da this conv writes, merged here, or null
 int launch_conv(const float *in, int cin, const float *wk, const float *bias, int cout, float *out, int B, bool acc,
-                hipStream_t st, const BnIn *bn = nullptr, float2 *stats = nullptr, const BnGrad *bg = nullptr,
+                hipStream_t st, const BnIn *bn = nullptr, const BnIn *bo = nullptr, const BnGrad *bg = nullptr,
                 const GradStats *gs = nullptr) {
     const int cinp = round4(cin);
-    const size_t lds = ((size_t)cinp * kPlane + 2 * 2304 + (bn || bg ? kBnStatFloats : 0)) * sizeof(float);
+    const size_t lds = ((size_t)cinp * kPlane + 2 * 2304 + (bn || bo || bg || gs ? kBnStatFloats + kLdsFlags : 0)) *
+                       sizeof(float);
     const int a = acc ? 1 : 0;
     const BnIn bn0{};
     const BnGrad bg0{};
     const GradStats gs0{};
     const BnIn &b = bn ? *bn : bn0;
+    const BnIn &o = bo ? *bo : bn0;
     const BnGrad &g = bg ? *bg : bg0;
     const GradStats &s = gs ? *gs : gs0;
-    const int mode = (bn ? kBnIn : 0) | (stats ? kStatsOut : 0) | (bg ? kBnGrad : 0) | (gs ? kGradStats : 0);
+    const int mode = (bn ? kBnIn : 0) | (bo ? kStatsOut : 0) | (bg ? kBnGrad : 0) | (gs ? kGradStats : 0);
+    // the hand-off counters are per channel slice
+    if ((bo || gs) && round16(cout) / 16 > kTickDbias) {
+        set_error("learner conv: %d output channels exceed the BatchNorm hand-off's slices", cout);
+        return SPAI_ERR_UNSUPPORTED;
+    }
 #define SPAI_CONV_CASE(C, M) \
-    case (C) * 16 + (M): return launch_conv_t<C, M>(B, lds, st, in, cin, wk, bias, cout, out, a, b, stats, g, s);
+    case (C) * 16 + (M): return launch_conv_t<C, M>(B, lds, st, in, cin, wk, bias, cout, out, a, b, o, g, s);
     switch (cinp * 16 + mode) {
     SPAI_CONV_CASE(4, 0)
     SPAI_CONV_CASE(4, kStatsOut)
@@ -1255,6 +1368,14 @@ static int learner_allreduce(spai_learner *L, float *buf, size_t n, hipStream_t 
     return SPAI_OK;
 }
 
+// carved from the end of bn_part: the bias-gradient partials, then the counters
+static float *learner_db_part(spai_learner *L, uint32_t B) {
+    return L->bn_part.p + (size_t)(2 * L->blocks + 3) * L->hidden * B * 2;
+}
+static unsigned *learner_ticks(spai_learner *L, uint32_t B) {
+    return (unsigned *)(learner_db_part(L, B) + (size_t)L->hidden * B);
+}
+
 // Everything of one train step after the batch upload: gradients zeroed, weights
 // packed, forward, loss, backward (weight gradients on the side streams), the cross-rank
 // reduction when there is a communicator, Adam.  Launch-only (no host sync).
@@ -1266,7 +1387,8 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
     // they got at learner_create
     const float eps = L->cfg.bn_eps, mom = L->cfg.bn_momentum;
     const size_t nl = L->convs.size();
-    k_pack_all<<<dim3(blocks_of((size_t)9 * 64 * 64), L->n_pack), kThreads, 0, st>>>(P, L->pack_desc.p, L->wt.p);
+    k_pack_all<<<dim3(blocks_of((size_t)9 * 64 * 64), L->n_pack), kThreads, 0, st>>>(P, L->pack_desc.p, L->wt.p,
+                                                                                        learner_ticks(L, B));
     const float *W = L->wt.p;
     const int pol = (int)nl - 2, val = (int)nl - 1;
 
@@ -1289,31 +1411,33 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
         const int last = 2 * L->blocks;   // the trunk's last conv
         auto part_of = [&](int l) { return (float2 *)L->bn_part.p + (size_t)l * L->hidden * B; };
         // layer l's BN input to its consumer: the residual is the block input a[l - 2] for a block's second conv
+        unsigned *tick = learner_ticks(L, B);
         auto bn_of = [&](int l) {
             const spai_learner::Conv &c = L->convs[l];
             const bool res = l >= 2 && l <= last && l % 2 == 0;
             return BnIn{part_of(l), P + c.g, P + c.be, res ? L->a[l - 2].p : nullptr, L->a[l].p, L->mean[l].p,
-                        L->invstd[l].p, P + c.mu, P + c.var, (int)B, eps, mom};
+                        L->invstd[l].p, P + c.mu, P + c.var, (int)B, eps, mom, tick};
         };
         {
             const spai_learner::Conv &c = L->convs[0];
-            crc = launch_conv(x_in, c.ci, W + c.wk, P + c.b, c.co, L->z[0].p, (int)B, false, st, nullptr, part_of(0));
+            const BnIn o = bn_of(0);
+            crc = launch_conv(x_in, c.ci, W + c.wk, P + c.b, c.co, L->z[0].p, (int)B, false, st, nullptr, &o);
         }
         for (int l = 1; l <= last && crc == SPAI_OK; ++l) {   // relu(h + BN(conv(relu(BN(conv(h)))))), model/mod.rs:152-165
             const spai_learner::Conv &c = L->convs[l];
-            const BnIn b = bn_of(l - 1);
-            crc = launch_conv(L->z[l - 1].p, c.ci, W + c.wk, P + c.b, c.co, L->z[l].p, (int)B, false, st, &b, part_of(l));
+            const BnIn b = bn_of(l - 1), o = bn_of(l);
+            crc = launch_conv(L->z[l - 1].p, c.ci, W + c.wk, P + c.b, c.co, L->z[l].p, (int)B, false, st, &b, &o);
         }
         if (crc == SPAI_OK) {   // the policy head conv applies the trunk's last BN and writes the trunk output
             const spai_learner::Conv &c = L->convs[pol];
-            const BnIn b = bn_of(last);
-            crc = launch_conv(L->z[last].p, c.ci, W + c.wk, P + c.b, c.co, L->z[pol].p, (int)B, false, st, &b,
-                              part_of(pol));
+            const BnIn b = bn_of(last), o = bn_of(pol);
+            crc = launch_conv(L->z[last].p, c.ci, W + c.wk, P + c.b, c.co, L->z[pol].p, (int)B, false, st, &b, &o);
         }
         h = L->a[last].p;
         if (crc == SPAI_OK) {
             const spai_learner::Conv &c = L->convs[val];
-            crc = launch_conv(h, c.ci, W + c.wk, P + c.b, c.co, L->z[val].p, (int)B, false, st, nullptr, part_of(val));
+            const BnIn o = bn_of(val);
+            crc = launch_conv(h, c.ci, W + c.wk, P + c.b, c.co, L->z[val].p, (int)B, false, st, nullptr, &o);
         }
         // the heads' BN + ReLU inside the loss kernel
         k_heads_loss<true><<<B, kThreads, 0, st>>>(L->z[pol].p, L->z[val].p, P + L->pol_w, P + L->pol_b, P + L->val_w,
@@ -1385,13 +1509,16 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
         const int last = 2 * L->blocks;
         auto gpart_of = [&](int l) { return (float2 *)L->bn_part.p + (size_t)l * L->hidden * B; };
         auto dzb_of = [&](int l) { return L->dzb.p + (size_t)(l - 1) * B * L->hidden * kCells; };   // l >= 1
+        unsigned *tick = learner_ticks(L, B);
+        float *db_part = learner_db_part(L, B);
         auto gs_of = [&](int l) {
-            return GradStats{L->a[l].p, L->z[l].p, L->mean[l].p, L->invstd[l].p, gpart_of(l)};
+            const spai_learner::Conv &c = L->convs[l];
+            return GradStats{L->a[l].p, L->z[l].p, L->mean[l].p, L->invstd[l].p, gpart_of(l), G + c.g, G + c.be, tick};
         };
         auto bg_of = [&](int l, float *dy_out) {
             const spai_learner::Conv &c = L->convs[l];
-            return BnGrad{gpart_of(l), L->a[l].p, L->z[l].p, L->mean[l].p, L->invstd[l].p, P + c.g, dzb_of(l), dy_out,
-                          G + c.g, G + c.be, (int)B};
+            return BnGrad{L->a[l].p, L->z[l].p, L->mean[l].p, L->invstd[l].p, P + c.g, G + c.g, G + c.be, dzb_of(l),
+                          dy_out, db_part, G + c.b, tick, (int)B};
         };
         {   // value head: its BN backward as before; its data gradient completes dL/d(trunk output)
             const spai_learner::Conv &c = L->convs[val];
@@ -1412,7 +1539,7 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
                 const BnGrad bgv = bg_of(l2, T);
                 const GradStats g = gs_of(l1);
                 crc = launch_conv(X, c.co, W + c.wkd, nullptr, c.ci, Y, (int)B, false, st, nullptr, nullptr, &bgv, &g);
-                wgrad_async(l2, L->a[l1].p, dzb_of(l2), G + c.b);
+                wgrad_async(l2, L->a[l1].p, dzb_of(l2));
             }
             if (crc == SPAI_OK) {   // conv 1: dz from Y, dx accumulated into T = dL/d(block input)
                 const spai_learner::Conv &c = L->convs[l1];
@@ -1420,7 +1547,7 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
                 const GradStats g = gs_of(l1 - 1);
                 crc = launch_conv(Y, c.co, W + c.wkd, nullptr, c.ci, T, (int)B, true, st, nullptr, nullptr, &bgv,
                                   l1 - 1 > 0 ? &g : nullptr);
-                wgrad_async(l1, hin, dzb_of(l1), G + c.b);
+                wgrad_async(l1, hin, dzb_of(l1));
             }
             float *nx = T;
             T = Y;

@@ -126,18 +126,18 @@ def test_bench_two_ranks_one_gpu(tmp_path):
     import sys
     from conftest import REPO
     G = 96
-    args = ["--sims", "32", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-isolated",
-            "--no-rules-bench", "--no-chess", "--no-timing"]
+    args = ["--sims", "32", "--steps", "2", "--warmup", "0", "--no-cpu-baseline", "--no-isolated",
+            "--no-rules-bench", "--no-chess", "--no-timing", "--no-lockstep-ref"]
     base = dict(os.environ, SPAI_BENCH_DEVICE="0")
 
-    def run(world, games):
+    def run(world, games, extra=()):
         with socket.socket() as s:
             s.bind(("127.0.0.1", 0))
             port = s.getsockname()[1]
         env = dict(base, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SPAI_GROUP_PORT=str(port),
                    WORLD_SIZE=str(world))
         procs = [subprocess.Popen([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(world),
-                                   "--games", str(games)] + args,
+                                   "--games", str(games)] + args + list(extra),
                                   env=dict(env, RANK=str(r), LOCAL_RANK=str(r)), stdout=subprocess.PIPE,
                                   stderr=subprocess.PIPE, text=True) for r in range(world)]
         try:
@@ -149,11 +149,16 @@ def test_bench_two_ranks_one_gpu(tmp_path):
         assert all(p.returncode == 0 for p in procs), [o[1][-2000:] for o in outs]
         return json.loads([l for l in outs[0][0].splitlines() if l.startswith("{")][-1])
 
+    # the default (streamed) schedule: 2 steps' games through the tree slots; the two
+    # ranks' id ranges [r k G, (r + 1) k G) cover the 1-rank run's [0, 2 k G); the
+    # lockstep schedule plays the same ids in batches of 2G, so its work is equal too
     one, two = run(1, 2 * G), run(2, G)
+    lock = run(1, 2 * G, ["--lockstep"])
     assert two["n_gpus"] == 2 and two["config"]["global_batch"] == 2 * G
     for k in ("sims", "evals", "games", "positions"):
-        assert two["work"][k] == one["work"][k], (k, one["work"], two["work"])
-    assert two["work"]["games"] == 2 * G
+        assert two["work"][k] == one["work"][k] == lock["work"][k], (k, one["work"], two["work"], lock["work"])
+    assert two["work"]["games"] == 2 * 2 * G
+    assert "streamed" in one["config"]["workload"] and "lockstep" in lock["config"]["workload"]
 
 
 def test_bench_gpus_flag_spawns_ranks():
@@ -170,7 +175,7 @@ def test_bench_gpus_flag_spawns_ranks():
     from conftest import REPO
     G = 96
     args = ["--sims", "32", "--steps", "1", "--warmup", "0", "--no-cpu-baseline", "--no-isolated",
-            "--no-rules-bench", "--no-chess", "--no-timing"]
+            "--no-rules-bench", "--no-chess", "--no-timing", "--no-lockstep-ref"]
     env = dict(os.environ, SPAI_BENCH_DEVICE="0")
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
