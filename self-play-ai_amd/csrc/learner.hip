@@ -1400,11 +1400,16 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
         k_bn_fwd<<<c.co, kBn, 0, st>>>(L->z[l].p, c.co, (int)B, eps, mom, L->mean[l].p, L->invstd[l].p, P + c.mu,
                                        P + c.var, P + c.g, P + c.be, res, L->a[l].p);
     };
-    // SPAI_LEARNER_BN_FUSE=0: a k_bn_fwd kernel after every conv (A/B knob); default:
-    // the trunk's BN + ReLU (+ residual) run inside the next conv's staging (BnIn)
+    // default: a k_bn_fwd kernel after every conv.  SPAI_LEARNER_BN_FUSE=1 (measured
+    // variant, not the default): the trunk's BN + ReLU (+ residual) run inside the
+    // next conv's staging (BnIn), the statistics merged inside the producer conv --
+    // 150-172k samples/s against 190-196k (profiles/r05/learner): at B = 128 a conv
+    // is a ~11 us, latency-bound launch, and the in-launch hand-off's drain, ticket
+    // and merge (or, merged in the consumer's prologue, every workgroup's read of
+    // the B partials) cost more than the k_bn_fwd / k_bn_bwd launches they remove
     static const bool fuse = [] {
         const char *v = std::getenv("SPAI_LEARNER_BN_FUSE");
-        return !v || std::atoi(v) != 0;
+        return v && std::atoi(v) != 0;
     }();
     const float *h = nullptr;
     if (fuse) {
@@ -1498,9 +1503,9 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
                                                                 G + L->val_w, G + L->val_b);
     k_linear_bwd_x<<<blocks_of((size_t)B * 3 * kCells), kThreads, 0, st>>>(L->dpre.p, P + L->val_w, (int)B, 1,
                                                                             3 * kCells, L->d1.p);
-    // SPAI_LEARNER_BNB_FUSE=0: a k_bn_bwd kernel before every data gradient (A/B knob);
-    // default (with the forward fusion): the trunk's BN backward runs in the data
-    // gradient's staging (BnGrad), its partials from the producer of da (GradStats)
+    // with the forward fusion on (SPAI_LEARNER_BN_FUSE=1), the trunk's BN backward runs in
+    // the data gradient's staging (BnGrad), its partials from the producer of da
+    // (GradStats), unless SPAI_LEARNER_BNB_FUSE=0 (a k_bn_bwd kernel before every data gradient)
     static const bool bfuse = [] {
         const char *v = std::getenv("SPAI_LEARNER_BNB_FUSE");
         return !v || std::atoi(v) != 0;

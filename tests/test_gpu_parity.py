@@ -740,9 +740,10 @@ def test_self_play_sampling_frequencies(spai):
 
 
 def test_learner_bn_fusion_matches_unfused(spai, tmp_path):
-    """the trunk's BatchNorm forward (BnIn) and backward (BnGrad) run inside the
-    neighbouring convs by default; SPAI_LEARNER_BN_FUSE=0 keeps one k_bn_fwd /
-    k_bn_bwd kernel per conv (read once per process, hence the subprocess).  Two
+    """SPAI_LEARNER_BN_FUSE=1 runs the trunk's BatchNorm forward (BnIn) and
+    backward (BnGrad) inside the neighbouring convs (a measured variant); the
+    default (=0) keeps one k_bn_fwd / k_bn_bwd kernel per conv (read once per
+    process, hence the subprocess).  Two
     Adam steps at 6 blocks x batch 128 from the same data: the two paths differ
     only in the summation order of the batch statistics (Chan's merge of
     per-sample partials against one two-pass sum), so the first step's losses
