@@ -13,13 +13,13 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 timeout -k 10 900 python bench.py --gpus 1 --steps ${STEPS:-20} --warmup ${WARMUP:-5} ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err; rc=$?; cat $O/bench.json | cut -c1-600; tail -3 $O/bench.err; [ $rc -eq 0 ] || exit $rc
 if [ -n "$PROFILE" ]; then
-  rm -rf /tmp/prof_b && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_b -o trace -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-isolated > $O/bench_under_rocprof.json 2> $O/bench_under_rocprof.err || { tail -5 $O/bench_under_rocprof.err; exit 1; }
+  rm -rf /tmp/prof_b && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_b -o trace -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-isolated --no-lockstep-ref > $O/bench_under_rocprof.json 2> $O/bench_under_rocprof.err || { tail -5 $O/bench_under_rocprof.err; exit 1; }
   find /tmp/prof_b -name '*kernel_stats.csv' -exec cp {} $O/trace_kernel_stats_two_chains.csv \;
   head -8 $O/trace_kernel_stats_two_chains.csv | cut -c1-160
   for c in FETCH_SIZE WRITE_SIZE; do
     rm -rf /tmp/pmc_$c
     timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d /tmp/pmc_$c -o p -- \
-      python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-isolated > $O/traffic_bench_$c.json 2> $O/traffic_bench_$c.err
+      python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-isolated --no-lockstep-ref > $O/traffic_bench_$c.json 2> $O/traffic_bench_$c.err
     rc=$?; echo "pass $c rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/traffic_bench_$c.err; exit $rc; }
   done
   python3 scripts/pmc_summary.py $O/forward_traffic.json $(find /tmp/pmc_FETCH_SIZE /tmp/pmc_WRITE_SIZE -name '*counter_collection*.csv') && grep -A5 '"k_forward<false>"' $O/forward_traffic.json
