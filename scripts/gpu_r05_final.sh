@@ -16,6 +16,7 @@ if [ -n "$PROFILE" ]; then
   rm -rf /tmp/prof_b && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_b -o trace -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-isolated --no-lockstep-ref > $O/bench_under_rocprof.json 2> $O/bench_under_rocprof.err || { tail -5 $O/bench_under_rocprof.err; exit 1; }
   find /tmp/prof_b -name '*kernel_stats.csv' -exec cp {} $O/trace_kernel_stats_two_chains.csv \;
   head -8 $O/trace_kernel_stats_two_chains.csv | cut -c1-160
+  t=$(find /tmp/prof_b -name '*kernel_trace.csv' | head -1); [ -n "$t" ] && python3 scripts/step_anatomy.py $t $O/anatomy.json > $O/anatomy.txt 2>&1; tail -5 $O/anatomy.txt
   for c in FETCH_SIZE WRITE_SIZE; do
     rm -rf /tmp/pmc_$c
     timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d /tmp/pmc_$c -o p -- \
