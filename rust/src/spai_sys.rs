@@ -145,6 +145,8 @@ extern "C" {
     pub fn spai_tree_use_subtree(e: *mut spai_engine, tree: u32, child_id: u32) -> c_int;
     pub fn spai_selfplay_run(e: *mut spai_engine, n_games: u32, game_id_base: u64, sink: spai_sample_sink,
                              user: *mut c_void, stats: *mut spai_selfplay_stats) -> c_int;
+    pub fn spai_selfplay_stream(e: *mut spai_engine, n_games: u32, window: u32, game_id_base: u64,
+                                sink: spai_sample_sink, user: *mut c_void, stats: *mut spai_selfplay_stats) -> c_int;
 
     // TicTacToe (game/tictactoe.rs, model/tictactoe.rs)
     pub fn spai_ttt_create(cfg: *const spai_config, device: c_int, out: *mut *mut spai_ttt) -> c_int;
