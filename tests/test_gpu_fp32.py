@@ -154,6 +154,40 @@ def test_f32_net_self_play_matches_oracle(spai, fixture):
 
 
 @pytest.mark.parametrize("fixture", FIXTURES)
+def test_f32_net_self_play_stream_matches_oracle(spai, fixture):
+    """spai_selfplay_stream with the fp32 net: the fixture's games through a third
+    as many tree slots (a slot takes the next game when its game ends).  Every
+    game's positions, visit policies, signed values and moves equal the oracle's
+    lockstep game of the same id; only the order of the games differs"""
+    z = _golden(fixture)
+    n, sims, seed = int(z["sp_games"]), int(z["sp_sims"]), int(z["sp_seed"])
+    e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_NET, seed=seed)
+    net = spai.Net(e, int(z["blocks"]), spai.init_params(int(z["blocks"]), 64, seed=int(z["seed"])),
+                   dtype=spai.DTYPE_F32)
+    e.set_net(net)
+    games, stats = e.self_play(n, window=max(2, n // 3))
+    ref = {}
+    k = 0
+    while k < len(z["sp_value"]):   # the fixture's games in emission order, by id
+        g = int(z["sp_game"][k])
+        m = 1
+        while k + m < len(z["sp_game"]) and int(z["sp_game"][k + m]) == g:
+            m += 1
+        ref[g] = (k, m)
+        k += m
+    assert sorted(g["game"] for g in games) == sorted(ref) and stats["games"] == n
+    for g in games:
+        k, m = ref[g["game"]]
+        assert len(g["value"]) == m
+        np.testing.assert_array_equal(g["policy"], z["sp_policy"][k:k + m])
+        np.testing.assert_array_equal(g["value"], z["sp_value"][k:k + m])
+        np.testing.assert_array_equal(g["enc"], z["sp_enc"][k:k + m])
+        assert list(g["moves"]) == list(z["sp_moves"][g["game"], :m])
+    net.close()
+    e.close()
+
+
+@pytest.mark.parametrize("fixture", FIXTURES)
 def test_f32_and_bf16_nets_agree_on_search(spai, fixture):
     """the bf16 throughput path against the fp32 path on the same roots: the root
     visit distributions are close (bf16 moves priors by ~1e-2, so visits may
