@@ -622,6 +622,107 @@ __global__ __launch_bounds__(kThreads) void k_conv_mfma(const float *__restrict_
     }
 }
 
+// k_conv_mfma<CINP, 1> (plain: no BatchNorm work) for SPW samples per workgroup:
+// workgroup (sample pair, 16-channel slice), the K split over the 4 waves as
+// there.  A wave's weight registers (its K part of the slice) serve every sample,
+// so a workgroup loads them once for SPW samples, and each k-step issues 3 SPW
+// MFMAs on one weight operand.  Samples past nsamp (odd batch) compute on a copy
+// of the last sample and store nothing.
+template <int CINP, int SPW>
+__global__ __launch_bounds__(kThreads) void k_conv_mfma_spw(const float *__restrict__ in, int cin,
+                                                            const float *__restrict__ wk,
+                                                            const float *__restrict__ bias, int cout, int coutp_all,
+                                                            float *__restrict__ out, int accumulate, int nsamp) {
+    constexpr int KS = 4, CSN = CINP / 4, KSTEPS = 9 * CSN, PER = KSTEPS / KS, MTS = 3;
+    static_assert(KSTEPS % KS == 0, "4 whole K parts");
+    extern __shared__ float sm[];
+    float *red = sm + SPW * CINP * kPlane;   // K-split partials [3 parts][SPW][3 mt][64 lanes][4]
+    const int lane = threadIdx.x & 63, part = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int s0 = part * PER, row = lane & 15, kq = lane >> 4;
+    const int co0 = 16 * (int)blockIdx.y;
+    const float *wl = wk + (size_t)(4 * s0 + kq) * coutp_all + co0 + row;
+    float bq[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) bq[i] = wl[(size_t)i * 4 * coutp_all];
+    int bs[SPW];
+#pragma unroll
+    for (int s = 0; s < SPW; ++s) {
+        const int b = (int)blockIdx.x * SPW + s;
+        bs[s] = b < nsamp ? b : nsamp - 1;
+        stage_planes_fast<CINP>(in + (size_t)bs[s] * cin * kCells, cin, sm + s * CINP * kPlane);
+    }
+    __syncthreads();
+    const float *xb[SPW][MTS];
+#pragma unroll
+    for (int s = 0; s < SPW; ++s)
+#pragma unroll
+        for (int mt = 0; mt < MTS; ++mt) {
+            const int p = mt * 16 + row, pp = p < kCells ? p : 0;
+            xb[s][mt] = sm + s * CINP * kPlane + kq * kPlane + (pp / kCols + 1) * 9 + pp % kCols + 1 - 10;
+        }
+    f32x4 acc[SPW][MTS];
+#pragma unroll
+    for (int s = 0; s < SPW; ++s)
+#pragma unroll
+        for (int mt = 0; mt < MTS; ++mt) acc[s][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto kloop = [&](auto part_c) {
+        constexpr int s0c = decltype(part_c)::value * PER;
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int k = s0c + i, tap = k / CSN, cs = k % CSN;
+            const int off = 4 * cs * kPlane + tap_off(tap) + 10;
+#pragma unroll
+            for (int s = 0; s < SPW; ++s)
+#pragma unroll
+                for (int mt = 0; mt < MTS; ++mt)
+                    acc[s][mt] = __builtin_amdgcn_mfma_f32_16x16x4f32(xb[s][mt][off], bq[i], acc[s][mt], 0, 0, 0);
+        }
+    };
+    if (part == 0) kloop(std::integral_constant<int, 0>{});
+    else if (part == 1) kloop(std::integral_constant<int, 1>{});
+    else if (part == 2) kloop(std::integral_constant<int, 2>{});
+    else kloop(std::integral_constant<int, 3>{});
+    if (part > 0) {
+        float *dst = red + ((size_t)(part - 1) * SPW * MTS * 64 + lane) * 4;
+#pragma unroll
+        for (int s = 0; s < SPW; ++s)
+#pragma unroll
+            for (int mt = 0; mt < MTS; ++mt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) dst[(s * MTS + mt) * 64 * 4 + r] = acc[s][mt][r];
+    }
+    __syncthreads();
+    if (part > 0) return;   // no barrier follows
+#pragma unroll
+    for (int q = 1; q < KS; ++q) {   // the fixed order of k_conv_mfma's sum
+        const float *src = red + ((size_t)(q - 1) * SPW * MTS * 64 + lane) * 4;
+#pragma unroll
+        for (int s = 0; s < SPW; ++s)
+#pragma unroll
+            for (int mt = 0; mt < MTS; ++mt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[s][mt][r] += src[(s * MTS + mt) * 64 * 4 + r];
+    }
+    const int n = co0 + row;
+    if (n >= cout) return;
+    const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int s = 0; s < SPW; ++s) {
+        if ((int)blockIdx.x * SPW + s >= nsamp) continue;
+        float *ob = out + ((size_t)bs[s] * cout + n) * kCells;
+#pragma unroll
+        for (int mt = 0; mt < MTS; ++mt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int p = mt * 16 + 4 * kq + r;
+                if (p < kCells) {
+                    const float v = acc[s][mt][r] + bv;
+                    ob[p] = accumulate ? ob[p] + v : v;
+                }
+            }
+    }
+}
+
 // weight-gradient partials: workgroup (chunk, group) accumulates, over the
 // kWgSamples samples of its chunk, the output tiles of its tile group:
 //   part[chunk][n][k] = sum_{b in chunk} sum_p dz[b][n][p] * X[b][p][k]   (k tap-major over CINP)
@@ -1115,6 +1216,12 @@ int learner_alloc_batch(spai_learner *L, uint32_t B) {
 // its own workgroup with the K split over its 4 waves (grid B x coutp/16: 4x
 // the workgroups of one per sample); the stem's input (4 padded channels, 9
 // k-steps) keeps one workgroup per sample with a wave per channel tile.
+// samples per workgroup of the plain convs (k_conv_mfma_spw; 1: k_conv_mfma)
+#ifndef SPAI_CONV_SPW
+#define SPAI_CONV_SPW 2
+#endif
+constexpr int kConvSpw = SPAI_CONV_SPW;
+
 template <int CINP, int MODE>
 int launch_conv_t(int B, size_t lds, hipStream_t st, const float *in, int cin, const float *wk, const float *bias,
                   int cout, float *out, int acc, const BnIn &bn, const BnIn &bo, const BnGrad &bg, const GradStats &gs) {
@@ -1130,6 +1237,12 @@ int launch_conv_t(int B, size_t lds, hipStream_t st, const float *in, int cin, c
     }
 #endif
     if constexpr (ks % 4 == 0) {
+        if constexpr (MODE == 0 && kConvSpw > 1) {   // plain conv: kConvSpw samples per workgroup
+            const size_t lds2 = ((size_t)kConvSpw * CINP * kPlane + (size_t)3 * kConvSpw * 3 * 64 * 4) * sizeof(float);
+            k_conv_mfma_spw<CINP, kConvSpw><<<dim3((B + kConvSpw - 1) / kConvSpw, nt), kThreads, lds2, st>>>(
+                in, cin, wk, bias, cout, 16 * nt, out, acc, B);
+            return SPAI_OK;
+        }
         k_conv_mfma<CINP, 1, MODE><<<dim3(B, nt), kThreads, lds, st>>>(in, cin, wk, bias, cout, 16 * nt, out, acc, bn,
                                                                       bo, bg, gs);
         return SPAI_OK;
