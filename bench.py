@@ -97,7 +97,7 @@ def parse():
     ap.add_argument("--chess-moves", type=int, default=2)
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events (A/B of their cost)")
     ap.add_argument("--no-isolated", action="store_true", help="skip the isolated-forward measurement")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r04", "final_b", "forward_traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r05", "final", "forward_traffic.json"),
                     help="PMC summary (scripts/gpu_traffic.sh) of this bench command: HBM bytes per k_forward launch")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
