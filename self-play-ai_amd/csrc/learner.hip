@@ -1216,9 +1216,13 @@ int learner_alloc_batch(spai_learner *L, uint32_t B) {
 // its own workgroup with the K split over its 4 waves (grid B x coutp/16: 4x
 // the workgroups of one per sample); the stem's input (4 padded channels, 9
 // k-steps) keeps one workgroup per sample with a wave per channel tile.
-// samples per workgroup of the plain convs (k_conv_mfma_spw; 1: k_conv_mfma)
+// samples per workgroup of the plain convs (1: k_conv_mfma; 2: k_conv_mfma_spw, a
+// measured variant: 12.7 against 10.9 us per conv, 181k against 189k samples/s --
+// its 272 registers leave one workgroup per CU, whose staging, k-loop and K-part
+// sum then run back to back instead of overlapping another workgroup's;
+// profiles/r05/learner/spw)
 #ifndef SPAI_CONV_SPW
-#define SPAI_CONV_SPW 2
+#define SPAI_CONV_SPW 1
 #endif
 constexpr int kConvSpw = SPAI_CONV_SPW;
 
