@@ -1692,7 +1692,12 @@ int net_eval_batch(spai_net *net, hipStream_t st, const uint32_t *d_count, uint3
         const char *v = std::getenv("SPAI_FWD_CONC");
         return !v || std::atoi(v) != 0;
     }();
-    k_forward<false><<<grid, kThreads, 0, st>>>(d_count, max_n, 0, conc_policy ? conc : 1, mine, theirs, nullptr,
+    // SPAI_FWD_S=k: every launch at group size k (A/B knob; the results do not depend on S)
+    static const int force_s = [] {
+        const char *v = std::getenv("SPAI_FWD_S");
+        return v ? std::max(0, std::min(kSRun, std::atoi(v))) : 0;
+    }();
+    k_forward<false><<<grid, kThreads, 0, st>>>(d_count, max_n, force_s, conc_policy ? conc : 1, mine, theirs, nullptr,
                                                 params_of(net), priors, value, nullptr);
     SPAI_HIP(hipGetLastError());
     return SPAI_OK;
