@@ -457,8 +457,14 @@ __global__ __launch_bounds__(64) void k_geo_init(const uint4 *__restrict__ geo, 
 #ifndef SPAI_DB4
 #define SPAI_DB4 2   // B ring at S = 4 (tuning knob)
 #endif
-__host__ __device__ constexpr int a_depth(int S) { return S <= 2 ? 9 : S <= 3 ? 6 : S <= 4 ? SPAI_DA4 : 3; }
-__host__ __device__ constexpr int b_depth(int S) { return S <= 2 ? 4 : S <= 3 ? 3 : S <= 4 ? SPAI_DB4 : 2; }
+#ifndef SPAI_DA8
+#define SPAI_DA8 3   // A ring at S >= 5 (tuning knob)
+#endif
+#ifndef SPAI_DB8
+#define SPAI_DB8 2   // B ring at S >= 5 (tuning knob)
+#endif
+__host__ __device__ constexpr int a_depth(int S) { return S <= 2 ? 9 : S <= 3 ? 6 : S <= 4 ? SPAI_DA4 : SPAI_DA8; }
+__host__ __device__ constexpr int b_depth(int S) { return S <= 2 ? 4 : S <= 3 ? 3 : S <= 4 ? SPAI_DB4 : SPAI_DB8; }
 
 // implicit-GEMM 3x3 conv over the LDS activations at IN for wave W's tasks.
 // Software pipeline: A (weights, global/L2) DA-1 k-steps ahead, B (LDS) DB-1
