@@ -1445,6 +1445,7 @@ void learner_destroy(spai_learner *L) {
     if (L->eng) (void)hipStreamSynchronize(L->eng->stream);
     for (hipStream_t ws : L->wg_stream)
         if (ws) (void)hipStreamSynchronize(ws);
+    if (L->graph) (void)hipGraphExecDestroy(L->graph);
     if (L->comm) (void)ncclCommDestroy((ncclComm_t)L->comm);
     for (hipEvent_t ev : L->ev_dz)
         if (ev) (void)hipEventDestroy(ev);
@@ -1745,9 +1746,33 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
     SPAI_HIP(hipMemcpyAsync(L->batch_in.p, L->stage, (nin + 2) * 4, hipMemcpyHostToDevice, st));
     const float *x_in = L->batch_in.p, *pi_in = x_in + (size_t)B * 3 * kCells, *z_in = pi_in + (size_t)B * 7;
     const float *bc = L->batch_in.p + nin;
-    // (a hipGraph of this step, captured once per batch size, measured 130k
-    // samples/s against 162k eager: profiles/r02/learner/graph_ab.txt)
-    SPAI_TRY(enqueue_step(L, B, st, x_in, pi_in, z_in, bc));
+    // SPAI_LEARNER_GRAPH=1 (measured variant): the step's launches captured once per
+    // batch size into a hipGraph and replayed (single-rank learners only: the host
+    // collective syncs inside the step).  Round 2 measured a capture at 130k
+    // samples/s against 162k eager (profiles/r02/learner/graph_ab.txt)
+    static const bool use_graph = [] {
+        const char *v = std::getenv("SPAI_LEARNER_GRAPH");
+        return v && std::atoi(v) != 0;
+    }();
+    if (use_graph && !L->comm && !L->host_ar) {
+        if (!L->graph || L->graph_batch != B) {
+            if (L->graph) (void)hipGraphExecDestroy(L->graph);
+            L->graph = nullptr;
+            hipGraph_t g = nullptr;
+            SPAI_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+            const int rc = enqueue_step(L, B, st, x_in, pi_in, z_in, bc);
+            const hipError_t ec = hipStreamEndCapture(st, &g);
+            SPAI_TRY(rc);
+            SPAI_CHECK(ec == hipSuccess && g, SPAI_ERR_DEVICE, "learner: step capture failed (%s)", hipGetErrorString(ec));
+            const hipError_t ei = hipGraphInstantiate(&L->graph, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            SPAI_CHECK(ei == hipSuccess, SPAI_ERR_DEVICE, "learner: graph instantiation failed (%s)", hipGetErrorString(ei));
+            L->graph_batch = B;
+        }
+        SPAI_HIP(hipGraphLaunch(L->graph, st));
+    } else {
+        SPAI_TRY(enqueue_step(L, B, st, x_in, pi_in, z_in, bc));
+    }
     L->last_batch = B;
     float *terms = L->stage + nin + 2;   // the staged inputs were consumed by the DMA above (stream order)
     SPAI_HIP(hipMemcpyAsync(terms, L->loss_terms.p, (size_t)B * 2 * 4, hipMemcpyDeviceToHost, st));

@@ -145,6 +145,8 @@ struct spai_learner {
     uint64_t step = 0;
     uint32_t max_batch = 0;
     uint32_t last_batch = 0;            // B of the latest train step (its activations stay in `a`)
+    hipGraphExec_t graph = nullptr;     // SPAI_LEARNER_GRAPH=1: the step captured once per batch size
+    uint32_t graph_batch = 0;
     size_t n_params = 0;
     struct Conv {
         int ci, co;
