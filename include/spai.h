@@ -527,6 +527,12 @@ typedef void (*spai_chess_sample_sink)(void *user, uint32_t game_id, uint32_t n,
                                        const uint16_t *moves /* [n] move played at each position */);
 int spai_chess_selfplay_run(spai_chess *e, uint32_t n_games, uint64_t game_id_base, spai_chess_sample_sink sink,
                             void *user, spai_selfplay_stats *stats);
+/* The same n_games chess games played through `window` tree slots (window <=
+ * max_trees), a finished game's slot taking the next game at once; every game
+ * identical to spai_chess_selfplay_run's (draws keyed by game id and the game's
+ * own move number), the sink sees games in the order they finish. */
+int spai_chess_selfplay_stream(spai_chess *e, uint32_t n_games, uint32_t window, uint64_t game_id_base,
+                               spai_chess_sample_sink sink, void *user, spai_selfplay_stats *stats);
 /* timing of the last search / self-play call, as spai_engine_timing:
  * ms[0] select + leaf rules, ms[1] net forward, ms[2] expand + backup */
 int spai_chess_set_timing(spai_chess *e, int enabled);

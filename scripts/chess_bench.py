@@ -52,6 +52,10 @@ def parse():
     ap.add_argument("--blocks", type=int, default=20)
     ap.add_argument("--moves", type=int, default=4)
     ap.add_argument("--full", action="store_true", help="play every game to completion (selfplay_run)")
+    ap.add_argument("--batches", type=int, default=1,
+                    help="--full: K x games games, as K lockstep batches or (--stream) one stream through the slots")
+    ap.add_argument("--stream", action="store_true",
+                    help="--full: the K x games games through `games` tree slots (spai_chess_selfplay_stream)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
@@ -169,8 +173,14 @@ def main():
     threading.Thread(target=heartbeat, args=(stop, t_start), daemon=True).start()
     rng = np.random.default_rng(args.seed)
     if args.full:
-        _, st = eng.self_play(args.games, keep=False)
-        sims, games, moves = st["sims"], st["games"], st["moves"]
+        sims = games = moves = 0
+        if args.stream:
+            _, st = eng.self_play(args.batches * args.games, keep=False, window=args.games)
+            sims, games, moves = st["sims"], st["games"], st["moves"]
+        else:
+            for k in range(args.batches):
+                _, st = eng.self_play(args.games, game_id_base=k * args.games, keep=False)
+                sims, games, moves = sims + st["sims"], games + st["games"], moves + st["moves"]
         dt = time.perf_counter() - t_start
     else:
         live = np.arange(args.games, dtype=np.uint32)
@@ -210,7 +220,9 @@ def main():
         "data": "synthetic: self-play from the start position, random-init net (tch default init, seed %d)" % args.seed,
         "config": {"workload": "chess self-play, %d games x %d sims/move, %dx256 ResNet bf16, %s"
                                % (args.games, args.sims, args.blocks,
-                                  "to completion" if args.full else "first %d moves" % moves),
+                                  ("%d games to completion%s" % (args.batches * args.games,
+                                                                 ", streamed through the slots" if args.stream else "")
+                                   if args.full else "first %d moves" % moves)),
                    "games": args.games, "sims_per_move": args.sims, "blocks": args.blocks},
         "seconds": dt, "moves": moves, "games_finished": games,
         "games_per_sec": games / dt if args.full else None,

@@ -317,6 +317,16 @@ int spai_chess_selfplay_run(spai_chess *e, uint32_t n_games, uint64_t game_id_ba
     return selfplay_run(e, n_games, game_id_base, sink, user, stats);
 }
 
+int spai_chess_selfplay_stream(spai_chess *e, uint32_t n_games, uint32_t window, uint64_t game_id_base,
+                               spai_chess_sample_sink sink, void *user, spai_selfplay_stats *stats) {
+    CH_CHECK(e);
+    if (window == 0) {
+        set_error("window must be > 0");
+        return SPAI_ERR_INVALID;
+    }
+    return selfplay_run(e, n_games, game_id_base, sink, user, stats, window);
+}
+
 int spai_chess_set_timing(spai_chess *e, int enabled) {
     CH_CHECK(e);
     KernelTimer &t = e->timer;

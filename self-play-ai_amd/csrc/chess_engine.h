@@ -140,6 +140,6 @@ int tree_root(spai_chess *e, uint32_t tree, spai_chess_state *root, uint32_t *vi
 int trees_advance(spai_chess *e, uint32_t n, const uint32_t *tree_idx, const uint32_t *child_index, uint8_t *status,
                   uint32_t *reps);
 int selfplay_run(spai_chess *e, uint32_t n_games, uint64_t gid_base, spai_chess_sample_sink sink, void *user,
-                 spai_selfplay_stats *stats);
+                 spai_selfplay_stats *stats, uint32_t window = 0);
 }  // namespace chess
 }  // namespace spai

@@ -351,9 +351,11 @@ __global__ __launch_bounds__(64 * kWavesPerBlock) void k_ccompact(TV T, const ui
     }
 }
 
-__global__ void k_ctrees_init(TV T, uint32_t n) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
+// every tree t < n (list null), or the n trees list[i], as a one-node tree at the start position
+__global__ void k_ctrees_init(TV T, uint32_t n, const uint32_t *__restrict__ list) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t t = list ? list[i] : i;
     const size_t base = (size_t)t * 2 * T.cap;
     T.nodes[base] = make_uint4(0u, 0u, 0u, 0u);
     T.first[base] = kNone;
@@ -582,7 +584,7 @@ int trees_create(spai_chess *e, uint32_t n) {
         SPAI_TRY(B.value.alloc(n));
         SPAI_TRY(e->active.alloc(n));
     }
-    k_ctrees_init<<<(n + 255) / 256, 256, 0, e->stream>>>(view(e), n);
+    k_ctrees_init<<<(n + 255) / 256, 256, 0, e->stream>>>(view(e), n, nullptr);
     SPAI_HIP(hipGetLastError());
     SPAI_HIP(hipStreamSynchronize(e->stream));
     return SPAI_OK;
@@ -783,15 +785,24 @@ int tree_root(spai_chess *e, uint32_t tree, spai_chess_state *root, uint32_t *vi
     return SPAI_OK;
 }
 
-// SelfPlayWorker::self_play (learner_concurrent.rs:169-242)
+// SelfPlayWorker::self_play (learner_concurrent.rs:169-242).  window < n_games
+// (spai_chess_selfplay_stream): the games run through `window` tree slots, a slot
+// whose game ended taking the next game (a fresh start-position tree) before the
+// next search; each game's draws are keyed by its id and its own move number, so
+// every game is the one the lockstep run plays.
 int selfplay_run(spai_chess *e, uint32_t n_games, uint64_t gid_base, spai_chess_sample_sink sink, void *user,
-                 spai_selfplay_stats *stats) {
+                 spai_selfplay_stats *stats, uint32_t window) {
     const auto t0 = std::chrono::steady_clock::now();
-    SPAI_CHECK(n_games >= 1 && n_games <= e->cfg.max_trees, SPAI_ERR_INVALID, "n_games %u (max_trees %u)", n_games,
+    const uint32_t W = (window == 0 || window >= n_games) ? n_games : window;   // tree slots
+    SPAI_CHECK(n_games >= 1 && W <= e->cfg.max_trees, SPAI_ERR_INVALID, "%u tree slots (max_trees %u)", W,
                e->cfg.max_trees);
-    SPAI_TRY(trees_create(e, n_games));
+    SPAI_TRY(trees_create(e, W));
     Trees &Tr = e->trees;
     const uint32_t sims = e->cfg.num_searches;
+    std::vector<uint32_t> slot_game(W), slot_move(W, 0);   // each slot's game (index < n_games) and its move number
+    for (uint32_t i = 0; i < W; ++i) slot_game[i] = i;
+    uint32_t next_game = W;
+    std::vector<uint32_t> refill;
     struct Rec {
         Board board;
         uint32_t reps;
@@ -799,11 +810,11 @@ int selfplay_run(spai_chess *e, uint32_t n_games, uint64_t gid_base, spai_chess_
         std::vector<uint32_t> vis;
         std::vector<uint16_t> mv;
     };
-    std::vector<std::vector<Rec>> hist(n_games);
-    std::vector<uint32_t> act(n_games);
-    for (uint32_t i = 0; i < n_games; ++i) act[i] = i;
-    std::vector<Board> roots(n_games);
-    std::vector<uint32_t> root_reps(n_games, 1);
+    std::vector<std::vector<Rec>> hist(W);
+    std::vector<uint32_t> act(W);
+    for (uint32_t i = 0; i < W; ++i) act[i] = i;
+    std::vector<Board> roots(W);
+    std::vector<uint32_t> root_reps(W, 1);
     for (auto &b : roots) start_board(b);
     double sims_done = 0, evals = 0, games = 0, positions = 0, moves = 0;
     uint64_t move_no = 0;
@@ -836,7 +847,7 @@ int selfplay_run(spai_chess *e, uint32_t n_games, uint64_t gid_base, spai_chess_
             const uint32_t *vis = Tr.h_visits.data() + (size_t)k * kMaxMoves;
             float fv[kMaxMoves];
             for (uint32_t j = 0; j < nch; ++j) fv[j] = (float)vis[j];
-            const float u = sample_u01_f32(e->cfg.seed, gid_base + t, move_no);
+            const float u = sample_u01_f32(e->cfg.seed, gid_base + slot_game[t], slot_move[t]++);
             const int idx = weighted_index(fv, (int)nch, e->cfg.temperature, u);
             SPAI_CHECK(idx >= 0, SPAI_ERR_NAN, "WeightedIndex over all-zero visits (the reference panics)");
             pick[k] = (uint32_t)idx;
@@ -887,13 +898,32 @@ int selfplay_run(spai_chess *e, uint32_t n_games, uint64_t gid_base, spai_chess_
                     val[h] = H[h].board.side == cur ? v : -v;
                     mvs[h] = H[h].move;
                 }
-                sink(user, (uint32_t)(gid_base + t), (uint32_t)m, enc.data(), pol.data(), val.data(), mvs.data());
+                sink(user, (uint32_t)(gid_base + slot_game[t]), (uint32_t)m, enc.data(), pol.data(), val.data(),
+                     mvs.data());
             }
             hist[t].clear();
             hist[t].shrink_to_fit();
         }
         for (uint32_t k = 0; k < na; ++k)
             if (!done[k]) keep.push_back(act[k]);
+        // streaming: the slots whose game ended take the next games (appended)
+        refill.clear();
+        for (uint32_t k = 0; k < na && next_game < n_games; ++k)
+            if (done[k]) {
+                const uint32_t t = act[k];
+                refill.push_back(t);
+                slot_game[t] = next_game++;
+                slot_move[t] = 0;
+                start_board(roots[t]);
+                root_reps[t] = 1;
+                keep.push_back(t);
+            }
+        if (!refill.empty()) {
+            const uint32_t nr = (uint32_t)refill.size();
+            SPAI_HIP(hipMemcpyAsync(e->active.p, refill.data(), 4 * nr, hipMemcpyHostToDevice, e->stream));
+            k_ctrees_init<<<(nr + 255) / 256, 256, 0, e->stream>>>(view(e), nr, e->active.p);
+            SPAI_HIP(hipGetLastError());
+        }
         act.swap(keep);
         ++move_no;
     }

@@ -48,7 +48,7 @@ SYMBOLS = [
     "spai_chess_move_index", "spai_chess_index_move", "spai_chess_net_num_params", "spai_chess_net_init_params",
     "spai_chess_net_create", "spai_chess_net_destroy", "spai_chess_net_forward", "spai_chess_predict", "spai_chess_set_net",
     "spai_chess_trees_create", "spai_chess_search", "spai_chess_tree_reset", "spai_chess_tree_use_subtree", "spai_chess_tree_root", "spai_chess_trees_advance",
-    "spai_chess_selfplay_run", "spai_chess_set_timing", "spai_chess_timing",
+    "spai_chess_selfplay_run", "spai_chess_selfplay_stream", "spai_chess_set_timing", "spai_chess_timing",
     # tictactoe (spai_ttt.py)
     "spai_ttt_create", "spai_ttt_destroy", "spai_ttt_games_resize", "spai_ttt_games_write", "spai_ttt_games_read",
     "spai_ttt_legal_mask", "spai_ttt_apply", "spai_ttt_encode", "spai_ttt_mask_invalid", "spai_ttt_net_num_params",

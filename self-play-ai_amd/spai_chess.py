@@ -63,6 +63,7 @@ def lib():
         L.spai_chess_tree_root.argtypes = [vp, u32, vp, vp, vp]
         L.spai_chess_trees_advance.argtypes = [vp, u32, vp, vp, vp, vp]
         L.spai_chess_selfplay_run.argtypes = [vp, u32, u64, SINK, vp, P(SelfPlayStats)]
+        L.spai_chess_selfplay_stream.argtypes = [vp, u32, u32, u64, SINK, vp, P(SelfPlayStats)]
         L.spai_chess_set_timing.argtypes = [vp, i32]
         L.spai_chess_timing.argtypes = [vp, vp, vp, vp]
         _ready = True
@@ -245,7 +246,9 @@ class ChessEngine:
         _check(lib().spai_chess_tree_root(self.h, tree, _p(st), C.byref(n), C.byref(w)))
         return st[0], n.value, w.value
 
-    def self_play(self, n_games, game_id_base=0, keep=True, keep_policy=True):
+    def self_play(self, n_games, game_id_base=0, keep=True, keep_policy=True, window=None):
+        """SelfPlayWorker::self_play over n_games games; window: play them through
+        that many tree slots (spai_chess_selfplay_stream), games in finishing order"""
         games = []
 
         def sink(user, gid, n, enc, pol, val, moves):
@@ -260,7 +263,10 @@ class ChessEngine:
 
         cb = SINK(sink)
         st = SelfPlayStats()
-        _check(lib().spai_chess_selfplay_run(self.h, n_games, game_id_base, cb, None, C.byref(st)))
+        if window is None:
+            _check(lib().spai_chess_selfplay_run(self.h, n_games, game_id_base, cb, None, C.byref(st)))
+        else:
+            _check(lib().spai_chess_selfplay_stream(self.h, n_games, int(window), game_id_base, cb, None, C.byref(st)))
         return games, {k: getattr(st, k) for k, _ in SelfPlayStats._fields_}
 
     def set_timing(self, on=True):

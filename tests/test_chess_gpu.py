@@ -306,6 +306,30 @@ def test_chess_self_play_hash_matches_oracle(ch, sc):
     eng.close()
 
 
+@pytest.mark.parametrize("window", [2, 4])
+def test_chess_self_play_stream_matches_oracle_per_game(ch, sc, window):
+    """spai_chess_selfplay_stream: the 6 games through `window` tree slots, a slot
+    taking the next game (a fresh start-position tree) when its game ends.  Every
+    game -- positions, visit policies, signed values, moves -- equals the oracle's
+    lockstep game of the same id; only the order in which games finish differs"""
+    n, sims, seed = 6, 8, 21
+    eng = sc.ChessEngine(num_searches=sims, max_trees=n, eval_kind=sc.EVAL_HASH, seed=seed, max_moves=2048)
+    games, stats = eng.self_play(n, game_id_base=0, window=window)
+    ref = ch.self_play(n, sims, seed=seed, max_plies=2048, with_policy=True)
+    assert sorted(g["game"] for g in games) == list(range(n))
+    for g in games:
+        rows = np.nonzero(ref["game"] == g["game"])[0]
+        assert len(rows) == g["n"] and np.all(np.diff(rows) == 1)
+        k, m = rows[0], g["n"]
+        assert np.array_equal(g["value"], ref["value"][k:k + m])
+        assert np.array_equal(g["enc"], ref["enc"][k:k + m])
+        assert np.array_equal(g["policy"], ref["policy"][k:k + m])
+        assert np.array_equal(g["moves"], ref["moves"][g["game"], :ref["n_moves"][g["game"]]].astype(np.uint16))
+    assert stats["games"] == n and stats["sims"] == ref["sims"] and stats["evals"] == ref["evals"]
+    ch.arena_reset()
+    eng.close()
+
+
 def test_chess_self_play_net_legal(ch, sc):
     n = 4
     eng = sc.ChessEngine(num_searches=6, max_trees=n, eval_kind=sc.EVAL_NET, seed=2, max_moves=2048)
