@@ -113,3 +113,14 @@ def test_parent_does_not_load_the_library(tmp_path):
     assert p.returncode != 0
     assert "rank exit status" in p.stderr
     assert "not built" in p.stderr   # the ranks, not the parent, reached the library
+
+
+def test_schedule_flags_parse(monkeypatch):
+    """the streamed schedule is the default; --lockstep selects one lockstep batch
+    per step; --stream (the round-5 A/B flag) still parses"""
+    sys.path.insert(0, REPO)
+    import bench
+    for argv, lock in (([], False), (["--lockstep"], True), (["--stream"], False)):
+        monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
+        a = bench.parse()
+        assert a.lockstep is lock and not a.no_lockstep_ref
