@@ -268,6 +268,12 @@ int spai_learner_destroy(spai_learner *l);
  * policies [n][7], values [n]; loss[3] = total, policy, value (may be NULL) */
 int spai_learner_train_batch(spai_learner *l, uint32_t n, const float *states, const float *policies,
                              const float *values, float *loss);
+/* k consecutive train steps of n samples each (step j reads rows [j n, (j+1) n)
+ * of the arrays): the same as k spai_learner_train_batch calls, with one host
+ * synchronisation at the end (the next batch is staged while a step runs);
+ * losses[3 k] = each step's total, policy, value (may be NULL) */
+int spai_learner_train_batches(spai_learner *l, uint32_t k, uint32_t n, const float *states, const float *policies,
+                               const float *values, float *losses);
 /* Model::train (model/mod.rs:100-149): a fresh Adam, one random permutation of
  * the n samples (keyed by seed), then `epochs` passes of ceil(n / batch) train
  * steps (the last batch may be short); loss[3] = the last step's */

@@ -60,6 +60,8 @@ def main():
     ap.add_argument("--batch", type=int, default=128)   # TrainingArgs::default (learner_concurrent.rs:61-69)
     ap.add_argument("--blocks", type=int, default=6)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--group", type=int, default=1,
+                    help="steps handed over per call (spai_learner_train_batches; 1: train_batch per step)")
     args = ap.parse_args()
     g = HostGroup()
     local = int(os.environ.get("SPAI_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0")))
@@ -75,8 +77,18 @@ def main():
     g.barrier()
     t0 = time.perf_counter()
     loss = None
-    for i in range(args.steps):
-        loss = L.train_batch(x[i % nb], pi[i % nb], z[i % nb])   # returns after the step (loss is read back)
+    if args.group <= 1:
+        for i in range(args.steps):
+            loss = L.train_batch(x[i % nb], pi[i % nb], z[i % nb])   # returns after the step (loss is read back)
+    else:   # the same steps, `group` per call (one host sync per call); the batches are prepared outside the clock
+        calls = []
+        for c0 in range(0, args.steps, args.group):
+            idx = [i % nb for i in range(c0, min(args.steps, c0 + args.group))]
+            calls.append((np.concatenate([x[i] for i in idx]), np.concatenate([pi[i] for i in idx]),
+                          np.concatenate([z[i] for i in idx]), len(idx)))
+        t0 = time.perf_counter()
+        for cx, cp, cz, k in calls:
+            loss = L.train_batches(cx, cp, cz, k)[-1]
     dt = time.perf_counter() - t0
     g.barrier()
     (dt_max,) = g.allreduce([dt], "max")
@@ -89,6 +101,7 @@ def main():
             "metric": "learner training samples/s (C4 train_batch: forward+backward+Adam)",
             "value": samples / dt_max, "unit": "samples/s", "n_gpus": g.world, "batch_per_gpu": args.batch,
             "steps": args.steps, "ms_per_step": dt_max * 1e3 / args.steps, "blocks": args.blocks,
+            "steps_per_call": max(1, args.group),
             "last_loss": [float(v) for v in loss], "replicas_identical": len(set(digests)) == 1,
             "collective": "RCCL all-reduce of %d fp32 gradients per step" % L.n if g.world > 1 else None,
             "roofline": {"bound": "fp32 vector", "achieved": ach, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -462,6 +462,16 @@ int spai_learner_train_batch(spai_learner *l, uint32_t n, const float *states, c
     return learner_train_batch(l, n, states, policies, values, loss);
 }
 
+int spai_learner_train_batches(spai_learner *l, uint32_t k, uint32_t n, const float *states, const float *policies,
+                               const float *values, float *losses) {
+    PTR_CHECK(l);
+    PTR_CHECK(states);
+    PTR_CHECK(policies);
+    PTR_CHECK(values);
+    ENG_CHECK(l->eng);
+    return learner_train_batches(l, k, n, states, policies, values, losses);
+}
+
 int spai_learner_params(spai_learner *l, float *params, size_t n) {
     PTR_CHECK(l);
     PTR_CHECK(params);

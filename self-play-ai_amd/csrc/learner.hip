@@ -1181,13 +1181,15 @@ int learner_alloc_batch(spai_learner *L, uint32_t B) {
     if (B <= L->max_batch) return SPAI_OK;
     const size_t act = (size_t)B * std::max(L->hidden, 32) * kCells;   // also the 32-channel policy head
     SPAI_TRY(L->batch_in.alloc((size_t)B * (3 * kCells + 8) + 2));
-    if (L->stage) (void)hipHostFree(L->stage);
-    L->stage = nullptr;
-    if (hipHostMalloc((void **)&L->stage, ((size_t)B * (3 * kCells + 10) + 2) * sizeof(float), hipHostMallocDefault) !=
-        hipSuccess) {
-        L->stage = nullptr;
-        set_error("learner: pinned staging allocation failed");
-        return SPAI_ERR_DEVICE;
+    for (float **h : {&L->stage, &L->stage_b}) {
+        if (*h) (void)hipHostFree(*h);
+        *h = nullptr;
+        if (hipHostMalloc((void **)h, ((size_t)B * (3 * kCells + 10) + 2) * sizeof(float), hipHostMallocDefault) !=
+            hipSuccess) {
+            *h = nullptr;
+            set_error("learner: pinned staging allocation failed");
+            return SPAI_ERR_DEVICE;
+        }
     }
     for (size_t l = 0; l < L->convs.size(); ++l) {
         SPAI_TRY(L->z[l].alloc((size_t)B * L->convs[l].co * kCells));
@@ -1416,6 +1418,11 @@ int learner_create(spai_engine *e, int blocks, int hidden, const float *params, 
             set_error("learner: stream/event creation failed");
             rc = SPAI_ERR_DEVICE;
         }
+    for (auto &ev : L->stage_ev)
+        if (rc == SPAI_OK && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            set_error("learner: event creation failed");
+            rc = SPAI_ERR_DEVICE;
+        }
     for (auto &ev : L->ev_dz)
         if (rc == SPAI_OK && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
             set_error("learner: event creation failed");
@@ -1456,6 +1463,10 @@ void learner_destroy(spai_learner *L) {
     }
     L->pack_desc.release();
     if (L->stage) (void)hipHostFree(L->stage);
+    if (L->stage_b) (void)hipHostFree(L->stage_b);
+    if (L->terms_host) (void)hipHostFree(L->terms_host);
+    for (hipEvent_t ev : L->stage_ev)
+        if (ev) (void)hipEventDestroy(ev);
     if (L->host_buf) (void)hipHostFree(L->host_buf);
     for (auto *b : {&L->p, &L->g, &L->bsum, &L->m, &L->v, &L->wt, &L->batch_in, &L->d0, &L->d1, &L->d2, &L->dzb, &L->bn_part, &L->dlogits,
                     &L->dpre, &L->loss_terms, &L->run_buf})
@@ -1729,27 +1740,27 @@ int enqueue_step(spai_learner *L, uint32_t B, hipStream_t st, const float *x_in,
     return SPAI_OK;
 }
 
-int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const float *policies, const float *values,
-                        float *loss3) {
-    SPAI_CHECK(B >= 1, SPAI_ERR_INVALID, "train_batch: empty batch");
-    SPAI_TRY(learner_alloc_batch(L, B));
+// one step's batch and Adam bias corrections into the pinned staging half `stage`,
+// one DMA of it, the step (eager, or the captured graph); launch-only
+static int stage_and_enqueue(spai_learner *L, uint32_t B, const float *states, const float *policies,
+                             const float *values, float *stage) {
     hipStream_t st = L->eng->stream;
-    // one DMA from pinned staging for the whole batch and this step's Adam bias corrections
     const size_t nin = (size_t)B * (3 * kCells + 8);
     L->step += 1;
     const double t = (double)L->step;
-    L->stage[nin] = (float)(1.0 - std::pow((double)L->cfg.beta1, t));
-    L->stage[nin + 1] = (float)std::sqrt(1.0 - std::pow((double)L->cfg.beta2, t));
-    std::memcpy(L->stage, states, (size_t)B * 3 * kCells * 4);
-    std::memcpy(L->stage + (size_t)B * 3 * kCells, policies, (size_t)B * 7 * 4);
-    std::memcpy(L->stage + (size_t)B * (3 * kCells + 7), values, (size_t)B * 4);
-    SPAI_HIP(hipMemcpyAsync(L->batch_in.p, L->stage, (nin + 2) * 4, hipMemcpyHostToDevice, st));
+    stage[nin] = (float)(1.0 - std::pow((double)L->cfg.beta1, t));
+    stage[nin + 1] = (float)std::sqrt(1.0 - std::pow((double)L->cfg.beta2, t));
+    std::memcpy(stage, states, (size_t)B * 3 * kCells * 4);
+    std::memcpy(stage + (size_t)B * 3 * kCells, policies, (size_t)B * 7 * 4);
+    std::memcpy(stage + (size_t)B * (3 * kCells + 7), values, (size_t)B * 4);
+    SPAI_HIP(hipMemcpyAsync(L->batch_in.p, stage, (nin + 2) * 4, hipMemcpyHostToDevice, st));
     const float *x_in = L->batch_in.p, *pi_in = x_in + (size_t)B * 3 * kCells, *z_in = pi_in + (size_t)B * 7;
     const float *bc = L->batch_in.p + nin;
     // SPAI_LEARNER_GRAPH=1 (measured variant): the step's launches captured once per
     // batch size into a hipGraph and replayed (single-rank learners only: the host
-    // collective syncs inside the step).  Round 2 measured a capture at 130k
-    // samples/s against 162k eager (profiles/r02/learner/graph_ab.txt)
+    // collective syncs inside the step).  Slower: the replay runs every kernel on one
+    // queue, so the weight gradients lose their overlap with the data-gradient chain
+    // (profiles/r05/learner/graph; round 2 likewise, profiles/r02/learner/graph_ab.txt)
     static const bool use_graph = [] {
         const char *v = std::getenv("SPAI_LEARNER_GRAPH");
         return v && std::atoi(v) != 0;
@@ -1774,19 +1785,66 @@ int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const 
         SPAI_TRY(enqueue_step(L, B, st, x_in, pi_in, z_in, bc));
     }
     L->last_batch = B;
-    float *terms = L->stage + nin + 2;   // the staged inputs were consumed by the DMA above (stream order)
-    SPAI_HIP(hipMemcpyAsync(terms, L->loss_terms.p, (size_t)B * 2 * 4, hipMemcpyDeviceToHost, st));
-    SPAI_HIP(hipStreamSynchronize(st));
-    double lp = 0, lv = 0;   // fixed-order host sums
+    return SPAI_OK;
+}
+
+// the fixed-order host sums of one step's loss terms
+static void sum_loss(const float *terms, uint32_t B, float *loss3) {
+    double lp = 0, lv = 0;
     for (uint32_t b = 0; b < B; ++b) {
         lp += terms[2 * b];
         lv += terms[2 * b + 1];
     }
-    if (loss3) {
-        loss3[1] = (float)(lp / B);
-        loss3[2] = (float)(lv / B);
-        loss3[0] = loss3[1] + loss3[2];
+    loss3[1] = (float)(lp / B);
+    loss3[2] = (float)(lv / B);
+    loss3[0] = loss3[1] + loss3[2];
+}
+
+int learner_train_batch(spai_learner *L, uint32_t B, const float *states, const float *policies, const float *values,
+                        float *loss3) {
+    SPAI_CHECK(B >= 1, SPAI_ERR_INVALID, "train_batch: empty batch");
+    SPAI_TRY(learner_alloc_batch(L, B));
+    hipStream_t st = L->eng->stream;
+    SPAI_TRY(stage_and_enqueue(L, B, states, policies, values, L->stage));
+    const size_t nin = (size_t)B * (3 * kCells + 8);
+    float *terms = L->stage + nin + 2;   // the staged inputs were consumed by the DMA above (stream order)
+    SPAI_HIP(hipMemcpyAsync(terms, L->loss_terms.p, (size_t)B * 2 * 4, hipMemcpyDeviceToHost, st));
+    SPAI_HIP(hipStreamSynchronize(st));
+    if (loss3) sum_loss(terms, B, loss3);
+    return SPAI_OK;
+}
+
+// k consecutive train steps of B samples each (batch j = rows [j B, (j + 1) B) of
+// the arrays), exactly k learner_train_batch calls, with one host synchronisation
+// at the end instead of one per step: step j + 1's batch is staged into the other
+// pinned half while step j runs (the half is refilled once its previous upload is
+// done), and every step's loss terms come back by a stream-ordered copy.
+// losses[3 j ..] = step j's {total, policy, value}.
+int learner_train_batches(spai_learner *L, uint32_t k, uint32_t B, const float *states, const float *policies,
+                          const float *values, float *losses) {
+    SPAI_CHECK(B >= 1 && k >= 1, SPAI_ERR_INVALID, "train_batches: need k >= 1 batches of B >= 1 samples");
+    SPAI_TRY(learner_alloc_batch(L, B));
+    hipStream_t st = L->eng->stream;
+    const size_t need = (size_t)k * B * 2;
+    if (L->terms_host_n < need) {
+        if (L->terms_host) (void)hipHostFree(L->terms_host);
+        L->terms_host = nullptr;
+        L->terms_host_n = 0;
+        SPAI_HIP(hipHostMalloc((void **)&L->terms_host, need * sizeof(float), hipHostMallocDefault));
+        L->terms_host_n = need;
     }
+    for (uint32_t j = 0; j < k; ++j) {
+        float *half = (j & 1) ? L->stage_b : L->stage;
+        if (j >= 2) SPAI_HIP(hipEventSynchronize(L->stage_ev[j & 1]));   // its previous upload is done
+        SPAI_TRY(stage_and_enqueue(L, B, states + (size_t)j * B * 3 * kCells, policies + (size_t)j * B * 7,
+                                   values + (size_t)j * B, half));
+        SPAI_HIP(hipEventRecord(L->stage_ev[j & 1], st));   // after the upload (and the step) in stream order
+        SPAI_HIP(hipMemcpyAsync(L->terms_host + (size_t)j * B * 2, L->loss_terms.p, (size_t)B * 2 * 4,
+                                hipMemcpyDeviceToHost, st));
+    }
+    SPAI_HIP(hipStreamSynchronize(st));
+    if (losses)
+        for (uint32_t j = 0; j < k; ++j) sum_loss(L->terms_host + (size_t)j * B * 2, B, losses + 3 * j);
     return SPAI_OK;
 }
 

@@ -162,6 +162,10 @@ struct spai_learner {
     int n_pack = 0;
     spai::DevBuf<float> batch_in;       // batch [x: B*126 | pi: B*7 | z: B]
     float *stage = nullptr;             // pinned host copy of it, then the loss terms [B*2]
+    float *stage_b = nullptr;           // a second staging half (learner_train_batches alternates)
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};   // each half's upload done
+    float *terms_host = nullptr;        // learner_train_batches: every step's loss terms (pinned)
+    size_t terms_host_n = 0;
     std::vector<spai::DevBuf<float>> z, a, mean, invstd;   // per conv layer
     spai::DevBuf<float> d0, d1;         // backward scratch [B][64][42]
     spai::DevBuf<float> bn_part;        // trunk convs' BN partials [layer][64][B] x 2 (forward: sum, centred sum
@@ -265,6 +269,8 @@ int learner_create(spai_engine *e, int blocks, int hidden, const float *params, 
 void learner_destroy(spai_learner *l);
 int learner_train_batch(spai_learner *l, uint32_t n, const float *states, const float *policies, const float *values,
                         float *loss3);
+int learner_train_batches(spai_learner *l, uint32_t k, uint32_t n, const float *states, const float *policies,
+                          const float *values, float *losses);
 int learner_activation(spai_learner *L, int layer, float *out, size_t n);
 int learner_params(spai_learner *l, float *params, size_t n, bool grads);
 int learner_train_epochs(spai_learner *l, uint32_t n, const float *states, const float *policies, const float *values,

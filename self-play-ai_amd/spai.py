@@ -34,7 +34,7 @@ SYMBOLS = [
     "spai_tree_reset", "spai_search", "spai_tree_use_subtree", "spai_tree_node", "spai_tree_size",
     "spai_selfplay_run", "spai_selfplay_stream", "spai_engine_set_timing", "spai_engine_timing", "spai_engine_timing_items",
     "spai_net_phase_cycles", "spai_net_bench", "spai_net_bench_conc", "spai_adam_config_default", "spai_learner_create", "spai_learner_destroy",
-    "spai_learner_train_batch", "spai_learner_params", "spai_learner_grads", "spai_learner_activation", "spai_comm_unique_id",
+    "spai_learner_train_batch", "spai_learner_train_batches", "spai_learner_params", "spai_learner_grads", "spai_learner_activation", "spai_comm_unique_id",
     "spai_learner_set_comm", "spai_learner_broadcast", "spai_learner_set_host_comm", "spai_learner_last_batch",
     "spai_comm_create", "spai_comm_allreduce_f64", "spai_comm_info", "spai_comm_destroy",
     "spai_params_save_safetensors", "spai_params_load_safetensors",
@@ -173,6 +173,7 @@ def lib():
         L.spai_learner_create.argtypes = [vp, i32, i32, vp, C.c_size_t, P(AdamConfig), P(vp)]
         L.spai_learner_destroy.argtypes = [vp]
         L.spai_learner_train_batch.argtypes = [vp, u32, vp, vp, vp, vp]
+        L.spai_learner_train_batches.argtypes = [vp, u32, u32, vp, vp, vp, vp]
         L.spai_learner_params.argtypes = [vp, vp, C.c_size_t]
         L.spai_learner_grads.argtypes = [vp, vp, C.c_size_t]
         L.spai_learner_activation.argtypes = [vp, C.c_int, vp, C.c_size_t]
@@ -472,6 +473,17 @@ class Learner:
         loss = np.zeros(3, np.float32)
         _check(lib().spai_learner_train_batch(self.h, len(x), _p(x), _p(pi), _p(z), _p(loss)))
         return loss   # total, policy, value
+
+    def train_batches(self, states, policies, values, k):
+        """k consecutive train_batch steps over equal slices of the arrays, one host
+        sync at the end; returns the k x 3 losses (total, policy, value)"""
+        x = np.ascontiguousarray(states, np.float32).reshape(-1, 126)
+        pi = np.ascontiguousarray(policies, np.float32).reshape(-1, 7)
+        z = np.ascontiguousarray(values, np.float32).reshape(-1)
+        assert len(x) == len(pi) == len(z) and k >= 1 and len(z) % k == 0
+        loss = np.zeros((k, 3), np.float32)
+        _check(lib().spai_learner_train_batches(self.h, k, len(z) // k, _p(x), _p(pi), _p(z), _p(loss)))
+        return loss
 
     def train(self, states, policies, values, epochs=1, batch=128, seed=0):
         """Model::train (model/mod.rs:100-149): fresh Adam, one permutation, epochs x batches"""

@@ -680,6 +680,35 @@ def test_pipeline_concurrent(spai, tmp_path):
     assert not np.array_equal(spai.load_params(str(tmp_path / "2.safetensors"), blocks), p0)
 
 
+def test_learner_train_batches_equals_single_steps(spai):
+    """spai_learner_train_batches(k) is k spai_learner_train_batch calls: the same
+    kernels in the same order, only the host synchronisation moves to the end, so
+    parameters and every step's losses are bit-identical (5 steps, batch 48, the
+    staging halves alternating and refilled twice)"""
+    blocks, B, k = 2, 48, 5
+    rng = np.random.default_rng(8)
+    n = B * k
+    states = _reachable_positions(spai, 3 * n, 10, seed=17)[:n]
+    e = spai.Engine(num_searches=1, max_trees=1)
+    e.games_resize(n)
+    e.games_write(states)
+    x = e.encode(n).reshape(n, 126)
+    pi = rng.random((n, 7)).astype(np.float32)
+    pi /= pi.sum(1, keepdims=True)
+    z = rng.choice(np.array([-1, 0, 1], np.float32), n)
+    p0 = spai.init_params(blocks, 64, seed=6)
+    one = spai.Learner(e, blocks, p0)
+    l1 = np.stack([one.train_batch(x[j * B:(j + 1) * B], pi[j * B:(j + 1) * B], z[j * B:(j + 1) * B])
+                   for j in range(k)])
+    grp = spai.Learner(e, blocks, p0)
+    l2 = grp.train_batches(x, pi, z, k)
+    np.testing.assert_array_equal(l1, l2)
+    np.testing.assert_array_equal(one.params(), grp.params())
+    one.close()
+    grp.close()
+    e.close()
+
+
 def test_learner_model_train_epochs(spai, oracle):
     """Model::train (model/mod.rs:100-149): a fresh Adam per call, one permutation of
     the samples, epochs x ceil(n/B) steps (short last batch) — vs the numpy oracle
