@@ -270,7 +270,8 @@ int spai_learner_train_batch(spai_learner *l, uint32_t n, const float *states, c
                              const float *values, float *loss);
 /* k consecutive train steps of n samples each (step j reads rows [j n, (j+1) n)
  * of the arrays): the same as k spai_learner_train_batch calls, with one host
- * synchronisation at the end (the next batch is staged while a step runs);
+ * synchronisation at the end (the next batch is staged while a step runs;
+ * measured no faster than k single calls: the step is GPU-bound);
  * losses[3 k] = each step's total, policy, value (may be NULL) */
 int spai_learner_train_batches(spai_learner *l, uint32_t k, uint32_t n, const float *states, const float *policies,
                                const float *values, float *losses);
