@@ -168,8 +168,9 @@ struct spai_learner {
     size_t terms_host_n = 0;
     std::vector<spai::DevBuf<float>> z, a, mean, invstd;   // per conv layer
     spai::DevBuf<float> d0, d1;         // backward scratch [B][64][42]
-    spai::DevBuf<float> bn_part;        // trunk convs' BN partials [layer][64][B] x 2 (forward: sum, centred sum
-                                        // of squares; backward: sum dy, sum dy xhat)
+    spai::DevBuf<float> bn_part;        // SPAI_LEARNER_BN_FUSE=1: the convs' BN partials [layer][64][B] x 2
+                                        // (forward: sum, centred sum of squares; backward: sum dy, sum dy xhat),
+                                        // then the bias-gradient partials [64][B] and the hand-off counters
     spai::DevBuf<float> dzb, d2;        // fused BN backward: dz of the trunk convs [2 blocks][B][64][42]; a third
                                         // activation-gradient buffer
     spai::DevBuf<float> dlogits, dpre, loss_terms;
