@@ -60,6 +60,34 @@ def test_c2_full_step_properties(spai, oracle):
     e.close()
 
 
+def test_c2_full_stream_equals_lockstep_per_game(spai):
+    """C2 at full size, the bench's streamed schedule against the lockstep one: 4096
+    games x 800 sims with the 6x64 bf16 net, once as one lockstep batch and once
+    through 2048 tree slots (a slot taking the next game when its game ends, so
+    the leaf batches, group sizes and chain splits all differ).  The forward does
+    not depend on its batch, and each game's draws are keyed by its id and its own
+    move number, so every game -- moves, visit policies, signed values, encodings
+    -- is bit-identical between the two schedules"""
+    G, sims = 4096, 800
+    e = spai.Engine(num_searches=sims, max_trees=G, eval_kind=spai.EVAL_NET, seed=0)
+    net = spai.Net(e, 6, spai.init_params(6, 64, seed=0))
+    e.set_net(net)
+    lock, st_l = e.self_play(G, game_id_base=7 * G)
+    strm, st_s = e.self_play(G, game_id_base=7 * G, window=G // 2)
+    for k in ("sims", "evals", "games", "positions"):
+        assert st_l[k] == st_s[k], (k, st_l, st_s)
+    by_id = {g["game"]: g for g in lock}
+    assert sorted(by_id) == sorted(g["game"] for g in strm) == list(range(7 * G, 8 * G))
+    for g in strm:
+        r = by_id[g["game"]]
+        assert list(g["moves"]) == list(r["moves"]), g["game"]
+        np.testing.assert_array_equal(g["policy"], r["policy"])
+        np.testing.assert_array_equal(g["value"], r["value"])
+        np.testing.assert_array_equal(g["enc"], r["enc"])
+    net.close()
+    e.close()
+
+
 def test_c4c_chess_two_moves_1024_trees(spai):
     import chessref
     import spai_chess as sc
