@@ -587,6 +587,9 @@ int spai_ttt_tree_use_subtree(spai_ttt *e, uint32_t tree, uint32_t child_index);
 /* SelfPlayWorker::self_play; the sink gets encodings [n][27], policies [n][9], values, moves */
 int spai_ttt_selfplay_run(spai_ttt *e, uint32_t n_games, uint64_t game_id_base, spai_sample_sink sink, void *user,
                           spai_selfplay_stats *stats);
+/* the same games through `window` tree slots (spai_selfplay_stream's contract) */
+int spai_ttt_selfplay_stream(spai_ttt *e, uint32_t n_games, uint32_t window, uint64_t game_id_base,
+                             spai_sample_sink sink, void *user, spai_selfplay_stats *stats);
 
 #ifdef __cplusplus
 }

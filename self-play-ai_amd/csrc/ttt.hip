@@ -925,24 +925,31 @@ int spai_ttt_tree_use_subtree(spai_ttt *e, uint32_t tree, uint32_t child_index) 
     return SPAI_OK;
 }
 
-// SelfPlayWorker::self_play (learner_concurrent.rs:169-242)
-int spai_ttt_selfplay_run(spai_ttt *e, uint32_t n_games, uint64_t gid_base, spai_sample_sink sink, void *user,
-                          spai_selfplay_stats *stats) {
-    T_CHECK(e);
+}  // extern "C"
+
+namespace {
+// SelfPlayWorker::self_play (learner_concurrent.rs:169-242); window < n_games: the
+// games through `window` tree slots, a slot whose game ended taking the next game
+// (a fresh empty-board tree), each game's draws keyed by its id and own move number
+int ttt_selfplay(spai_ttt *e, uint32_t n_games, uint64_t gid_base, spai_sample_sink sink, void *user,
+                 spai_selfplay_stats *stats, uint32_t window) {
     const auto t0 = std::chrono::steady_clock::now();
-    SPAI_TRY(trees_create(e, n_games));
+    const uint32_t W = (window == 0 || window >= n_games) ? n_games : window;   // tree slots
+    SPAI_TRY(trees_create(e, W));
     const uint32_t sims = e->cfg.num_searches;
+    std::vector<uint32_t> slot_game(W), slot_move(W, 0);
+    for (uint32_t i = 0; i < W; ++i) slot_game[i] = i;
+    uint32_t next_game = W;
     struct Rec {
         State s;
         float pol[9];
         int32_t move;
     };
-    std::vector<std::vector<Rec>> hist(n_games);
-    std::vector<uint32_t> act(n_games);
-    std::vector<State> roots(n_games, State{0, 0, 0, 0});
-    for (uint32_t i = 0; i < n_games; ++i) act[i] = i;
+    std::vector<std::vector<Rec>> hist(W);
+    std::vector<uint32_t> act(W);
+    std::vector<State> roots(W, State{0, 0, 0, 0});
+    for (uint32_t i = 0; i < W; ++i) act[i] = i;
     double sims_done = 0, evals = 0, games = 0, positions = 0, moves = 0;
-    uint64_t move_no = 0;
     std::vector<uint32_t> st, pick, cnt;
     std::vector<State> nb;
     while (!act.empty()) {
@@ -963,7 +970,7 @@ int spai_ttt_selfplay_run(spai_ttt *e, uint32_t n_games, uint64_t gid_base, spai
             Rec r;
             r.s = roots[t];
             visit_policy(roots[t], s, r.pol, nullptr, vis);
-            const float u = sample_u01_f32(e->cfg.seed, gid_base + t, move_no);
+            const float u = sample_u01_f32(e->cfg.seed, gid_base + slot_game[t], slot_move[t]++);
             const int idx = weighted_index(vis, (int)s[0], e->cfg.temperature, u);
             SPAI_CHECK(idx >= 0, SPAI_ERR_NAN, "WeightedIndex over all-zero visits (the reference panics)");
             pick[k] = (uint32_t)idx;
@@ -997,15 +1004,25 @@ int spai_ttt_selfplay_run(spai_ttt *e, uint32_t n_games, uint64_t gid_base, spai
                     val[h] = x_to_move(H[h].s.n) == cur_x ? v : -v;
                     mv[h] = H[h].move;
                 }
-                sink(user, (uint32_t)(gid_base + t), (uint32_t)m, enc.data(), pol.data(), val.data(), mv.data());
+                sink(user, (uint32_t)(gid_base + slot_game[t]), (uint32_t)m, enc.data(), pol.data(), val.data(),
+                     mv.data());
             }
             hist[t].clear();
         }
         std::vector<uint32_t> keep;
         for (uint32_t k = 0; k < na; ++k)
             if (!done[k]) keep.push_back(act[k]);
+        for (uint32_t k = 0; k < na && next_game < n_games; ++k)   // streaming: refill the ended games' slots
+            if (done[k]) {
+                const uint32_t t = act[k];
+                slot_game[t] = next_game++;
+                slot_move[t] = 0;
+                roots[t] = State{0, 0, 0, 0};
+                k_ttree_reset<<<1, 1, 0, e->stream>>>(view(e), t, roots[t]);
+                SPAI_HIP(hipGetLastError());
+                keep.push_back(t);
+            }
         act.swap(keep);
-        ++move_no;
     }
     if (stats) {
         stats->sims = sims_done;
@@ -1016,6 +1033,22 @@ int spai_ttt_selfplay_run(spai_ttt *e, uint32_t n_games, uint64_t gid_base, spai
         stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }
     return SPAI_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int spai_ttt_selfplay_run(spai_ttt *e, uint32_t n_games, uint64_t gid_base, spai_sample_sink sink, void *user,
+                          spai_selfplay_stats *stats) {
+    T_CHECK(e);
+    return ttt_selfplay(e, n_games, gid_base, sink, user, stats, 0);
+}
+
+int spai_ttt_selfplay_stream(spai_ttt *e, uint32_t n_games, uint32_t window, uint64_t gid_base, spai_sample_sink sink,
+                             void *user, spai_selfplay_stats *stats) {
+    T_CHECK(e);
+    SPAI_CHECK(window > 0, SPAI_ERR_INVALID, "window must be > 0");
+    return ttt_selfplay(e, n_games, gid_base, sink, user, stats, window);
 }
 
 }  // extern "C"

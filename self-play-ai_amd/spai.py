@@ -55,7 +55,7 @@ SYMBOLS = [
     "spai_ttt_net_init_params", "spai_ttt_net_create", "spai_ttt_net_destroy", "spai_ttt_net_forward",
     "spai_ttt_predict",
     "spai_ttt_set_net", "spai_ttt_trees_create", "spai_ttt_search", "spai_ttt_tree_reset", "spai_ttt_tree_use_subtree",
-    "spai_ttt_selfplay_run",
+    "spai_ttt_selfplay_run", "spai_ttt_selfplay_stream",
 ]
 COMM_ID_BYTES = 128
 

@@ -40,6 +40,7 @@ def lib():
         L.spai_ttt_tree_use_subtree.argtypes = [vp, u32, u32]
         L.spai_ttt_tree_reset.argtypes = [vp, u32, vp]
         L.spai_ttt_selfplay_run.argtypes = [vp, u32, u64, SINK, vp, P(SelfPlayStats)]
+        L.spai_ttt_selfplay_stream.argtypes = [vp, u32, u32, u64, SINK, vp, P(SelfPlayStats)]
         _ready = True
     return L
 
@@ -150,7 +151,9 @@ class TTTEngine:
     def use_subtree(self, tree, child_index):
         _check(lib().spai_ttt_tree_use_subtree(self.h, tree, child_index))
 
-    def self_play(self, n_games, game_id_base=0):
+    def self_play(self, n_games, game_id_base=0, window=None):
+        """SelfPlayWorker::self_play; window: through that many tree slots
+        (spai_ttt_selfplay_stream), games in finishing order"""
         games = []
 
         def sink(user, gid, n, enc, pol, val, moves):
@@ -161,7 +164,10 @@ class TTTEngine:
 
         cb = SINK(sink)
         st = SelfPlayStats()
-        _check(lib().spai_ttt_selfplay_run(self.h, n_games, game_id_base, cb, None, C.byref(st)))
+        if window is None:
+            _check(lib().spai_ttt_selfplay_run(self.h, n_games, game_id_base, cb, None, C.byref(st)))
+        else:
+            _check(lib().spai_ttt_selfplay_stream(self.h, n_games, int(window), game_id_base, cb, None, C.byref(st)))
         return games, {k: getattr(st, k) for k, _ in SelfPlayStats._fields_}
 
 

@@ -156,6 +156,28 @@ def test_ttt_self_play_hash_matches_oracle(oracle, st):
     eng.close()
 
 
+@pytest.mark.parametrize("window", [5, 11])
+def test_ttt_self_play_stream_matches_oracle_per_game(oracle, st, window):
+    """spai_ttt_selfplay_stream: the 24 games through `window` tree slots; every
+    game (positions, visit policies, signed values, moves) equals the oracle's
+    lockstep game of the same id, only the finishing order differs"""
+    n, sims, seed = 24, 32, 7
+    eng = st.TTTEngine(num_searches=sims, max_trees=n, eval_kind=st.EVAL_HASH, seed=seed)
+    games, stats = eng.self_play(n, window=window)
+    ref = oracle.self_play(oracle.GAME_TICTACTOE, n, sims, seed, eval_kind=oracle.EVAL_HASH, max_plies=9)
+    assert sorted(g["game"] for g in games) == list(range(n))
+    for g in games:
+        rows = np.nonzero(ref["game"] == g["game"])[0]
+        k, m = int(rows[0]), len(rows)
+        assert m == g["n"] and np.all(np.diff(rows) == 1)
+        assert np.array_equal(g["enc"], ref["enc"][k:k + m])
+        assert np.array_equal(g["policy"], ref["policy"][k:k + m])
+        assert np.array_equal(g["value"], ref["value"][k:k + m])
+        assert np.array_equal(g["moves"], ref["moves"][g["game"], :ref["n_moves"][g["game"]]])
+    assert stats["games"] == n and stats["sims"] == ref["sims"] and stats["evals"] == ref["evals"]
+    eng.close()
+
+
 def test_ttt_config1_self_play_with_net(oracle, st):
     # BASELINE config 1: one game, 64 sims/move, random-init 2-block net
     eng = st.TTTEngine(num_searches=64, max_trees=1, eval_kind=st.EVAL_NET, seed=1)
