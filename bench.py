@@ -335,6 +335,14 @@ def rccl_comm(dist, spai):
         return None, "RCCL communicator failed: %r" % (ex,)
 
 
+def stream_base(first, k, world, rank, G):
+    """first game id of rank `rank`'s stream of k steps' games starting at step
+    `first`: the ranks' ranges [(first * world + rank * k) * G, + k * G) tile
+    [first * world * G, (first + k) * world * G) without overlap (world 1: the
+    ids of lockstep steps first .. first + k - 1)"""
+    return (first * world + rank * k) * G
+
+
 def main():
     args = parse()
     if args.cpu_baseline_only:
@@ -362,9 +370,8 @@ def main():
         return st
 
     def stream(first, k):
-        """k steps' worth of games through G tree slots; rank r plays ids
-        [(first * world + r * k) * G, + k * G) (world 1: the lockstep steps' ids)"""
-        base = (first * dist.world + dist.rank * k) * G
+        """k steps' worth of games through G tree slots (stream_base)"""
+        base = stream_base(first, k, dist.world, dist.rank, G)
         _, st = eng.self_play(k * G, game_id_base=base, collect=False, window=G)
         return st
 

@@ -124,3 +124,26 @@ def test_schedule_flags_parse(monkeypatch):
         monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
         a = bench.parse()
         assert a.lockstep is lock and not a.no_lockstep_ref
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_stream_game_ids_partition(world):
+    """the streamed bench's game ids: the ranks' ranges tile the job's range with no
+    overlap, the warm-up stream's ids are disjoint from the timed region's, and at
+    world 1 the stream plays the lockstep steps' ids (step i: [i G, (i + 1) G))"""
+    sys.path.insert(0, REPO)
+    import bench
+    G, k, w = 96, 3, 2
+
+    def ids(first, steps):
+        out = []
+        for r in range(world):
+            b = bench.stream_base(first, steps, world, r, G)
+            out.extend(range(b, b + steps * G))
+        return out
+
+    timed, warm = ids(0, k), ids(-w, w)
+    assert sorted(timed) == list(range(0, k * world * G))
+    assert sorted(warm) == list(range(-w * world * G, 0))
+    if world == 1:
+        assert timed == [g for i in range(k) for g in range(i * G, (i + 1) * G)]
