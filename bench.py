@@ -73,8 +73,8 @@ def weight_bytes(blocks):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--games", type=int, default=4096, help="parallel self-play games per GPU")
     ap.add_argument("--sims", type=int, default=800, help="MCTS simulations per move")
     ap.add_argument("--blocks", type=int, default=6)
