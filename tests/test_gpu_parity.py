@@ -429,6 +429,29 @@ def test_self_play_device_sampling_matches_oracle(spai, oracle, temperature):
     e.close()
 
 
+@pytest.mark.parametrize("temperature,window", [(0.7, 29), (3.0, 50)])
+def test_self_play_stream_temperature_matches_oracle(spai, oracle, temperature, window):
+    """spai_selfplay_stream at temperatures other than the default, twice on the
+    same engine (the visits^T table reused; a second game-id base): each game is
+    the oracle's lockstep game of the same id bit for bit"""
+    n, sims, seed = 72, 24, 5
+    e = spai.Engine(num_searches=sims, max_trees=n, eval_kind=spai.EVAL_HASH, seed=seed, temperature=temperature)
+    for base in (0, 1000):
+        games, stats = e.self_play(n, game_id_base=base, window=window)
+        ref = oracle.self_play(oracle.GAME_CONNECT4, n, sims, seed, eval_kind=oracle.EVAL_HASH, max_plies=42,
+                               temperature=temperature, game_id_base=base)
+        assert sorted(g["game"] for g in games) == list(range(base, base + n))
+        for g in games:
+            rows = np.nonzero(ref["game"] + base == g["game"])[0]
+            k, m = int(rows[0]), len(rows)
+            assert m == len(g["value"]) and np.all(np.diff(rows) == 1)
+            np.testing.assert_array_equal(g["policy"], ref["policy"][k:k + m])
+            np.testing.assert_array_equal(g["value"], ref["value"][k:k + m])
+            np.testing.assert_array_equal(g["enc"], ref["enc"][k:k + m])
+        assert stats["sims"] == ref["sims"] and stats["games"] == n
+    e.close()
+
+
 kTailChunk = 4   # search.hip: passes per host check
 
 
