@@ -44,6 +44,7 @@ Adds to the JSON line:
 import argparse
 import json
 import os
+import resource
 import subprocess
 import sys
 import time
@@ -99,6 +100,15 @@ def parse():
     ap.add_argument("--no-isolated", action="store_true", help="skip the isolated-forward measurement")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r05", "final", "forward_traffic.json"),
                     help="PMC summary (scripts/gpu_traffic.sh) of this bench command: HBM bytes per k_forward launch")
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r06", "final", "forward_pmc.json"),
+                    help="PMC summary of this bench command (scripts/gpu_roofline_pmc.sh): executed MFMA FLOPs, MFMA "
+                         "busy cycles and HBM bytes per k_forward launch; preferred over --traffic-json when present")
+    ap.add_argument("--chess-cpu-seconds", type=float, default=15.0,
+                    help="the chess window's CPU leg: this many seconds of the chess oracle's tree loop + libtorch "
+                         "CPU 20x256 (scripts/chess_bench.py --cpu-baseline-only)")
+    ap.add_argument("--chess-cpu-games", type=int, default=16)
+    ap.add_argument("--chess-record", default=os.path.join(REPO, "profiles", "r06", "chess_full", "record.json"),
+                    help="committed record of BASELINE config 4 played to completion (scripts/chess_bench.py --full)")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -207,7 +217,7 @@ def rules_bench(eng):
     return out
 
 
-def chess_window(args, device):
+def chess_window(args, device, dist_world=1):
     """BASELINE config 4 (chess, 1024 games x 400 sims/move, 20x256 bf16) for the first
     --chess-moves moves from the start position: every move searches every live tree,
     samples visits^1.25 and re-roots (scripts/chess_bench.py, windowed).  sims/s and
@@ -245,13 +255,38 @@ def chess_window(args, device):
     fpe = cb.flops_per_eval(blocks)
     leaves = items[1] / max(1.0, launches[1])
     tf = fpe * leaves / (ms[1] * 1e-3) / 1e12 if ms[1] > 0 else None
-    return {"workload": "chess self-play, %d games x %d sims/move, %dx256 ResNet bf16, first %d moves from the "
-                        "start position" % (games, sims, blocks, args.chess_moves),
-            "sims_per_sec": done / dt, "seconds": dt,
-            "forward": {"kernel": "k_chess_forward", "avg_launch_ms": ms[1], "avg_leaves_per_launch": leaves,
-                        "flop_per_eval": fpe, "achieved_TFLOP/s": tf,
-                        "frac": tf / BF16_PEAK_TFLOPS if tf else None},
-            "kernel_ms": {"select_leaf": ms[0], "forward": ms[1], "expand": ms[2]}}
+    out = {"workload": "chess self-play, %d games x %d sims/move, %dx256 ResNet bf16, first %d moves from the "
+                       "start position" % (games, sims, blocks, args.chess_moves),
+           "sims_per_sec": done / dt, "seconds": dt,
+           "forward": {"kernel": "k_chess_forward", "avg_launch_ms": ms[1], "avg_leaves_per_launch": leaves,
+                       "flop_per_eval": fpe, "achieved_TFLOP/s": tf,
+                       "frac": tf / BF16_PEAK_TFLOPS if tf else None},
+           "kernel_ms": {"select_leaf": ms[0], "forward": ms[1], "expand": ms[2]}}
+    out["record"] = chess_record(args.chess_record)
+    if dist_world == 1 and args.chess_cpu_seconds > 0:
+        # the CPU reference path on the same window's shape: the chess oracle's tree loop
+        # (AoS arena, a full State per node, sequential descent) + libtorch CPU fp32 20x256,
+        # from the start position, run in a subprocess (torch never enters this process)
+        ns = argparse.Namespace(cpu_seconds=args.chess_cpu_seconds, cpu_games=args.chess_cpu_games, blocks=blocks,
+                                seed=args.seed, cpu_threads=0)
+        c = cb.run_cpu_baseline(ns)
+        out["cpu_baseline"] = c
+        if c.get("value"):
+            out["vs_cpu"] = out["sims_per_sec"] / c["value"]
+    return out
+
+
+def chess_record(path):
+    """the committed full-game record of BASELINE config 4 (scripts/chess_bench.py --full,
+    profiles/r06/chess_full): games/s and sims/s of 2 x 1024 games played to completion at
+    400 sims/move, lockstep and streamed, flagged with the commit it was taken at"""
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+    except (OSError, ValueError):
+        return None
+    rec["source"] = os.path.relpath(path, REPO)
+    return rec
 
 
 def _free_port():
@@ -330,9 +365,21 @@ def rccl_comm(dist, spai):
     try:
         with _StdoutToStderr():
             uid = dist.g.broadcast_bytes(spai.comm_unique_id() if dist.rank == 0 else None)
-            return spai.Comm(dist.local, dist.rank, dist.world, uid), None
-    except Exception as ex:   # reported in the line; the host group still carries the reductions
-        return None, "RCCL communicator failed: %r" % (ex,)
+            comm = spai.Comm(dist.local, dist.rank, dist.world, uid)
+    except Exception as ex:
+        if dist.world > 1:   # the peers may be blocked inside ncclCommInitRank (no timeout): exit so the
+            rank_fail("RCCL communicator failed on rank %d: %r" % (dist.rank, ex))   # launcher stops them
+        return None, "RCCL communicator failed: %r" % (ex,)   # 1 rank: reported in the line
+    if dist.world > 1 and not all(dist.g.allgather(True)):   # every rank formed it before any collective
+        rank_fail("RCCL communicator: not every rank formed it")
+    return comm, None
+
+
+def rank_fail(msg):
+    """a rank of an N > 1 run that cannot go on: exit non-zero at once, so spawn_ranks (or
+    the launcher) stops the other ranks instead of leaving them in an RCCL collective"""
+    print("bench.py: " + msg, file=sys.stderr, flush=True)
+    os._exit(3)
 
 
 def stream_base(first, k, world, rank, G):
@@ -388,6 +435,7 @@ def main():
     # 4th measured ~5 %: 31.9M vs 33.4M sims/s), ~1000 sampled launches per step
     eng.set_timing(not args.no_timing, stride=32)
     tot = dict(sims=0.0, games=0.0, evals=0.0, positions=0.0, moves=0.0)
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     if streaming:
         st = stream(0, args.steps)
@@ -399,9 +447,17 @@ def main():
             for k in tot:
                 tot[k] += st[k]
     eng.sync()
+    t_own = time.perf_counter() - t0   # this rank's own work, before it waits for the others
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
     dist.barrier()
     dt = time.perf_counter() - t0
     timing = eng.timing()
+    # host CPU time of this rank's process (every thread: the self-play host loop, the HIP
+    # runtime's) over the timed region: the host-core budget per GPU
+    cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+    per_rank = dist.g.allgather({"rank": dist.rank, "device": dist.local, "wall_s": t_own, "sims": tot["sims"],
+                                 "games": tot["games"], "sims_per_sec": tot["sims"] / t_own,
+                                 "host_cpu_s": cpu_s, "host_cpu_share": cpu_s / t_own})
     (dt_max,) = dist.reduce([dt], "max")
     counters = [tot["sims"], tot["games"], tot["evals"], tot["positions"]]
     sims, games, evals, positions = dist.reduce(counters, "sum")
@@ -414,7 +470,11 @@ def main():
             rccl = {"ranks": comm.info()[1], "devices": dist.g.allgather(dist.local),
                     "counters_agree": r_sum == [sims, games, evals, positions] and r_max == dt_max}
         except Exception as ex:
+            if dist.world > 1:
+                rank_fail("RCCL all-reduce failed on rank %d: %r" % (dist.rank, ex))
             rccl = {"ranks": 0, "note": "RCCL all-reduce failed: %r" % (ex,)}
+        if dist.world > 1 and not all(dist.g.allgather(True)):
+            rank_fail("RCCL all-reduce: not every rank completed it")
         with _StdoutToStderr():
             comm.close()
 
@@ -422,8 +482,17 @@ def main():
     ev = timing["evaluate"]
     achieved = fpe * ev["items"] / (ev["total_ms"] * 1e-3) / 1e12 if ev["total_ms"] > 0 else None
     per_launch_flop = fpe * ev["items"] / ev["launches"] if ev["launches"] else None
-    traffic, traffic_src = None, None
-    if os.path.exists(args.traffic_json):   # measured by separate rocprofv3 --pmc passes of this command
+    traffic, traffic_src, pmc = None, None, None
+    if os.path.exists(args.pmc_json):   # rocprofv3 --pmc passes of this command (scripts/gpu_roofline_pmc.sh)
+        with open(args.pmc_json) as f:
+            pmc = json.load(f)
+        kf = pmc.get("k_forward<false>", {})
+        if "hbm_bytes_per_launch" in kf:
+            traffic = kf["hbm_bytes_per_launch"]
+            traffic_src = ("%s: (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch over %d launches (FETCH doubled for "
+                           "gfx950), commit %s" % (os.path.relpath(args.pmc_json, REPO), kf["launches"],
+                                                  pmc.get("commit", "?")))
+    if traffic is None and os.path.exists(args.traffic_json):   # measured by separate rocprofv3 --pmc passes of this command
         with open(args.traffic_json) as f:
             tj = json.load(f)
         if "k_forward<false>" in tj:
@@ -431,6 +500,22 @@ def main():
             traffic_src = ("%s: (2*FETCH_SIZE + WRITE_SIZE)*1024 per launch over %d launches "
                            "(FETCH doubled for gfx950)" % (os.path.relpath(args.traffic_json, REPO),
                                                            tj["k_forward<false>"]["launches"]))
+    executed = None
+    if pmc and "derived" in pmc:
+        d = pmc["derived"]
+        frac_job = evals / dt_max * fpe / 1e12 / dist.world / BF16_PEAK_TFLOPS
+        executed = {
+            "executed_over_algorithmic": d["executed_over_algorithmic"],
+            # the job-level rate in the FLOPs the MFMA pipe actually executes (tap skipping drops the
+            # MFMAs of all-off-board (tile, tap) pairs; padding rows add some)
+            "executed_flop_frac": frac_job * d["executed_over_algorithmic"],
+            "mfma_busy": d["mfma_busy"],
+            "mfma_insts_per_launch": d["mfma_insts_per_launch"],
+            "wave_cycles": d.get("wave_cycles"),
+            "source": "%s (commit %s): SQ_INSTS_MFMA x 16*16*32*2 per k_forward launch over the launch's "
+                      "algorithmic FLOPs (its leaves x flop_per_eval); mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / "
+                      "(GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs) per launch under rocprofv3 (kernels serialised)"
+                      % (os.path.relpath(args.pmc_json, REPO), pmc.get("commit", "?"))}
     result = {
         "metric": METRIC,
         "value": sims / dt_max,
@@ -452,8 +537,17 @@ def main():
                    "model": "c4-resnet-%dx64" % args.blocks, "games_per_gpu": G, "sims_per_move": args.sims,
                    "global_batch": G * dist.world, "parallelism": "dp%d (games sharded, no collective)" % dist.world},
         "work": {"sims": sims, "games": games, "evals": evals, "positions": positions},   # summed over ranks
+        "schedule": "streamed" if streaming else "lockstep",
         "rccl_ranks": rccl["ranks"],
         "rccl": rccl,
+        "per_rank": per_rank,
+        "host": {"cpu_s_per_rank_max": max(r["host_cpu_s"] for r in per_rank),
+                 "cpu_share_per_rank_max": max(r["host_cpu_share"] for r in per_rank),
+                 "cores_per_node_at_8_ranks": 8 * max(r["host_cpu_share"] for r in per_rank),
+                 "sims_per_sec_rank_spread": (max(r["sims_per_sec"] for r in per_rank) /
+                                              min(r["sims_per_sec"] for r in per_rank)),
+                 "note": "host CPU seconds (getrusage of each rank process: user + system, all threads) over the "
+                         "timed region; share = CPU seconds / the rank's own wall time, i.e. host cores busy per GPU"},
         "evals_per_sec": evals / dt_max,
         "positions_per_sec": positions / dt_max,
         "kernel_ms": {k: v["avg_ms"] for k, v in timing.items()},
@@ -464,6 +558,7 @@ def main():
                      "basis": "job level: flop_per_eval x leaves evaluated in the timed region / its wall time, "
                               "per GPU (the two search chains' forwards overlap, so per-launch event times "
                               "over-count the step; see per_launch)",
+                     "executed": executed,
                      "traffic": traffic,
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                      # algorithmic bytes of one launch: the packed bf16 weights + fp32 biases once,
@@ -480,17 +575,22 @@ def main():
     }
     # the lockstep schedule beside the streamed headline: one step of G games started
     # together (game ids after the timed region's), rank 0 of a 1-rank run
-    if streaming and dist.rank == 0 and dist.world == 1 and not args.no_lockstep_ref:
+    if streaming and not args.no_lockstep_ref:   # every rank, its own game ids after the timed region's
         eng.set_timing(False)
         eng.sync()
+        dist.barrier()
         t1 = time.perf_counter()
         ls = step(args.steps)
         eng.sync()
-        d1 = time.perf_counter() - t1
-        result["lockstep"] = {"value": ls["sims"] / d1, "games_per_sec": ls["games"] / d1, "ms_per_step": d1 * 1e3,
-                              "frac": ls["evals"] / d1 * fpe / 1e12 / BF16_PEAK_TFLOPS, "steps": 1,
-                              "note": "one batch of %d games started together and played to completion "
-                                      "(the reference worker's schedule; bench.py --lockstep times K of these)" % G}
+        dist.barrier()
+        (d1,) = dist.reduce([time.perf_counter() - t1], "max")
+        ls_sims, ls_games, ls_evals = dist.reduce([ls["sims"], ls["games"], ls["evals"]], "sum")
+        result["lockstep"] = {"value": ls_sims / d1, "games_per_sec": ls_games / d1, "ms_per_step": d1 * 1e3,
+                              "frac": ls_evals / d1 * fpe / 1e12 / dist.world / BF16_PEAK_TFLOPS, "steps": 1,
+                              "n_gpus": dist.world,
+                              "note": "one batch of %d games per GPU started together and played to completion "
+                                      "(the reference worker's schedule; bench.py --lockstep times K of these); "
+                                      "summed over ranks, max time" % G}
     # the same forward launch ALONE on the GPU (spai_net_bench, HIP events, random reachable
     # positions) at the timed region's mean leaves per launch, at one chain's (x2) and at the
     # full-batch sizes: the isolated-kernel roofline beside the shared-CU per-launch figure above
@@ -521,7 +621,7 @@ def main():
     eng.close()
     if not args.no_chess and dist.rank == 0:
         try:
-            result["chess"] = chess_window(args, dist.local)
+            result["chess"] = chess_window(args, dist.local, dist.world)
         except Exception as ex:   # the window must never sink the headline number
             result["chess"] = {"error": repr(ex)[:300]}
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:

@@ -223,7 +223,9 @@ int spai_engine_timing_items(spai_engine *eng, double *total_ms, double *items);
  * epilogue end, barrier passed).  Wall clock (s_memrealtime): cycles[20] = shader
  * cycles from kernel entry to the first group's start, [21] the same in ns, [22] ns
  * from the first group's start to the workgroup's end, [23] ns from the earliest
- * entry to the latest end over the launch.  cycles holds 24 doubles.  Needs the
+ * entry to the latest end over the launch.  cycles holds 24 doubles (48 in the
+ * k-step diagnostic build, SPAI_DIAG_KSTEP: [24 + ks] after k-step ks of block 1
+ * conv 1, [42] before its barrier, [43] after it, [44] its start).  Needs the
  * diagnostic build (SPAI_DIAG); the production library returns
  * SPAI_ERR_UNSUPPORTED.  Never on the timed path. */
 int spai_net_phase_cycles(spai_net *net, uint32_t count, double *cycles);

@@ -36,7 +36,7 @@ struct Gpu {
     net: *mut sys::spai_net,
     max_trees: u32,
     num_searches: u32,
-    fingerprint: (f64, f64),
+    fingerprint: Option<u64>,
 }
 // the handles are used by one thread at a time (one engine per self-play worker, main.rs:169-186)
 unsafe impl Send for Gpu {}
@@ -64,7 +64,7 @@ struct Trainer {
     // VarStore fingerprint after the learner's last write-back: a different one
     // means the trainer's variables were changed from outside (VarStore::load /
     // copy), and the learner is rebuilt from them rather than overwriting them
-    fingerprint: (f64, f64),
+    fingerprint: Option<u64>,
 }
 unsafe impl Send for Trainer {}
 
@@ -175,7 +175,7 @@ impl Net {
         let n = z.len();
         assert!(x.len() == n * 126 && pi.len() == n * 7, "train batch shapes: [n][3][6][7], [n][7], [n](x1)");
         let mut g = self.trainer.lock().unwrap();
-        if g.as_ref().map_or(false, |t| t.fingerprint != self.fingerprint()) {
+        if g.as_ref().map_or(false, |t| t.fingerprint != Some(self.fingerprint())) {
             *g = None;   // Drop destroys the stale learner and its engine
         }
         if g.is_none() {
@@ -192,7 +192,7 @@ impl Net {
             sys::check(unsafe {
                 sys::spai_learner_create(e, self.blocks as i32, 64, p.as_ptr(), p.len(), std::ptr::null(), &mut l)
             });
-            *g = Some(Trainer { engine: e, learner: l, n_params: p.len(), fingerprint: (f64::NAN, f64::NAN) });
+            *g = Some(Trainer { engine: e, learner: l, n_params: p.len(), fingerprint: None });
         }
         let t = g.as_mut().unwrap();
         let mut loss = [0f32; 3];
@@ -210,7 +210,7 @@ impl Net {
             off += k;
         }
         assert_eq!(off, p.len(), "VarStore variables vs the device learner's flat parameters");
-        t.fingerprint = self.fingerprint();
+        t.fingerprint = Some(self.fingerprint());
         loss[0] as f64
     }
 }
@@ -225,11 +225,11 @@ impl Net {
         p
     }
 
-    fn fingerprint(&self) -> (f64, f64) {
-        let _g = tch::no_grad_guard();
-        self.vars.iter().fold((0.0, 0.0), |(s, a), t| {
-            (s + t.sum(Kind::Double).double_value(&[]), a + t.abs().sum(Kind::Double).double_value(&[]))
-        })
+    /// bit-exact fingerprint of the VarStore's values (model/mod.rs `fingerprint`: panics
+    /// on a NaN or infinite parameter, so a diverged model is reported rather than the
+    /// device learner being rebuilt, and its Adam state reset, on every step)
+    fn fingerprint(&self) -> u64 {
+        super::fingerprint(&self.vars)
     }
 
     /// the device engine (at least `trees` trees; `num_searches` per search, None =
@@ -253,10 +253,10 @@ impl Net {
             let mut e = std::ptr::null_mut();
             sys::check(unsafe { sys::spai_engine_create(sys::SPAI_GAME_CONNECT4, &cfg, device, &mut e) });
             *g = Some(Gpu { engine: e, net: std::ptr::null_mut(), max_trees: cfg.max_trees, num_searches,
-                                fingerprint: (f64::NAN, f64::NAN) });
+                                fingerprint: None });
         }
         let d = g.as_mut().unwrap();
-        if d.net.is_null() || d.fingerprint != fp {
+        if d.net.is_null() || d.fingerprint != Some(fp) {
             let p = self.params();
             let dtype = if std::env::var("SPAI_DTYPE").as_deref() == Ok("f32") { sys::SPAI_DTYPE_F32 } else { sys::SPAI_DTYPE_BF16 };
             let mut net = std::ptr::null_mut();
@@ -265,7 +265,7 @@ impl Net {
                 unsafe { sys::spai_net_destroy(d.net) };
             }
             d.net = net;
-            d.fingerprint = fp;
+            d.fingerprint = Some(fp);
             sys::check(unsafe { sys::spai_engine_set_net(d.engine, net) });
         }
         g

@@ -203,13 +203,22 @@ pub(crate) fn flat_params(vars: &[Tensor]) -> Vec<f32> {
     p
 }
 
-/// (sum, sum of |x|) over the variables: changes whenever the VarStore's values do,
-/// so a device copy of the weights is rebuilt after a trainer -> self-play copy
-pub(crate) fn fingerprint(vars: &[Tensor]) -> (f64, f64) {
+/// bit-exact fingerprint of the variables' values: FNV-1a over every f32 bit pattern in
+/// construction order, so a device copy of the weights is rebuilt after any trainer ->
+/// self-play copy or VarStore::load.  A NaN or infinite value panics: a diverged model is
+/// reported (the reference panics on NaN too, quirk Q11) instead of every call rebuilding
+/// the device copy, since a NaN fingerprint would never equal itself
+pub(crate) fn fingerprint(vars: &[Tensor]) -> u64 {
     let _g = tch::no_grad_guard();
-    vars.iter().fold((0.0, 0.0), |(s, a), t| {
-        (s + t.sum(Kind::Double).double_value(&[]), a + t.abs().sum(Kind::Double).double_value(&[]))
-    })
+    let mut h = 0xcbf2_9ce4_8422_2325u64;
+    for t in vars {
+        let v = Vec::<f32>::try_from(t.to_device(Device::Cpu).to_kind(Kind::Float).contiguous().view(-1)).unwrap();
+        assert!(v.iter().all(|x| x.is_finite()), "a model parameter is NaN or infinite (training diverged)");
+        for x in v {
+            h = (h ^ x.to_bits() as u64).wrapping_mul(0x0000_0100_0000_01b3);
+        }
+    }
+    h
 }
 
 /// the GPU the nets' engines run on (SPAI_DEVICE, default 0)

@@ -39,7 +39,7 @@ struct Gpu {
     net: *mut sys::spai_ttt_net,
     max_trees: u32,
     num_searches: u32,
-    fingerprint: (f64, f64),
+    fingerprint: Option<u64>,
 }
 // used by one thread at a time (one Mcts + Model per self-play worker, main.rs:169-186)
 unsafe impl Send for Gpu {}
@@ -207,10 +207,10 @@ impl Net {
             let mut e = std::ptr::null_mut();
             sys::check(unsafe { sys::spai_ttt_create(&cfg, super::device_index(), &mut e) });
             *g = Some(Gpu { engine: e, net: std::ptr::null_mut(), max_trees: cfg.max_trees, num_searches,
-                            fingerprint: (f64::NAN, f64::NAN) });
+                            fingerprint: None });
         }
         let d = g.as_mut().unwrap();
-        if d.net.is_null() || d.fingerprint != fp {
+        if d.net.is_null() || d.fingerprint != Some(fp) {
             let p = super::flat_params(&self.vars);
             let mut net = std::ptr::null_mut();
             sys::check(unsafe { sys::spai_ttt_net_create(d.engine, self.blocks as i32, p.as_ptr(), p.len(), &mut net) });
@@ -218,7 +218,7 @@ impl Net {
                 unsafe { sys::spai_ttt_net_destroy(d.net) };
             }
             d.net = net;
-            d.fingerprint = fp;
+            d.fingerprint = Some(fp);
             sys::check(unsafe { sys::spai_ttt_set_net(d.engine, net) });
         }
         g

@@ -11,7 +11,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FPE = 39016572
 
 
-def one(counts, iters, blocks):
+def one(counts, iters, blocks, conc=1):
     sys.path.insert(0, os.path.join(REPO, "self-play-ai_amd"))
     import spai
     e = spai.Engine(num_searches=1, max_trees=1)
@@ -19,7 +19,7 @@ def one(counts, iters, blocks):
     net.bench(max(counts), iters=max(1, int(0.2e6 / 120 / 1)))   # ~0.2 s of launches: settle the clock first
     out = {}
     for n in counts:
-        ms = net.bench(n, iters=iters)
+        ms = net.bench(n, iters=iters, conc=conc)
         out[n] = ms
     net.close()
     e.close()
@@ -32,17 +32,18 @@ def main():
     ap.add_argument("--counts", default="1,64,256,512,768,1024,1280,1536,1792,2048,3072,4096")
     ap.add_argument("--iters", type=int, default=300)
     ap.add_argument("--blocks", type=int, default=6)
+    ap.add_argument("--conc", type=int, default=1, help="group size for this many concurrent chains (spai_net_bench_conc)")
     ap.add_argument("--child", action="store_true")
     a = ap.parse_args()
     counts = [int(c) for c in a.counts.split(",")]
     if a.child:
-        one(counts, a.iters, a.blocks)
+        one(counts, a.iters, a.blocks, a.conc)
         return
     libs = a.libs.split(",") if a.libs else [os.environ.get("SPAI_LIB", os.path.join(REPO, "self-play-ai_amd", "libspai.so"))]
     for lib in libs:
         env = dict(os.environ, SPAI_LIB=lib)
         r = subprocess.run([sys.executable, __file__, "--child", "--counts", a.counts, "--iters", str(a.iters),
-                            "--blocks", str(a.blocks)], env=env, capture_output=True, text=True, timeout=300)
+                            "--blocks", str(a.blocks), "--conc", str(a.conc)], env=env, capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
             print(lib, "FAILED", r.stderr[-800:])
             sys.exit(1)

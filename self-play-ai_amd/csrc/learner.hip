@@ -1773,7 +1773,10 @@ static int stage_and_enqueue(spai_learner *L, uint32_t B, const float *states, c
             SPAI_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
             const int rc = enqueue_step(L, B, st, x_in, pi_in, z_in, bc);
             const hipError_t ec = hipStreamEndCapture(st, &g);
-            SPAI_TRY(rc);
+            if (rc != SPAI_OK || ec != hipSuccess) {   // a failed capture: free the partial graph before returning
+                if (g) (void)hipGraphDestroy(g);
+                SPAI_TRY(rc);
+            }
             SPAI_CHECK(ec == hipSuccess && g, SPAI_ERR_DEVICE, "learner: step capture failed (%s)", hipGetErrorString(ec));
             const hipError_t ei = hipGraphInstantiate(&L->graph, g, nullptr, nullptr, 0);
             (void)hipGraphDestroy(g);

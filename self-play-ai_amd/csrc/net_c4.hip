@@ -110,7 +110,12 @@ constexpr int kLdsBytes = kPart + kWaves * kSplitMaxN * 1024;
 constexpr int kSRun = kS;
 constexpr int kLdsBytes = kTab + 42 * 16;
 #endif
+#ifdef SPAI_DIAG_KSTEP
+constexpr int kStamps = 48;                // + 24..41: after each k-step of block 1 conv 1, 42 before its barrier, 43
+                                           // after it, 44 at its start (diagnostic k-step build)
+#else
 constexpr int kStamps = 24;                // phase stamps per wave in the diagnostic mode (17..19: inside block 0 conv1;
+#endif
                                            // 20/21: s_memtime / s_memrealtime at kernel entry, 22: s_memrealtime at the
                                            // first group's stamp 0, 23: s_memrealtime after the last group)
 static_assert(kS * kLinPitch * 2 <= kHBytes, "head features fit in Y");
@@ -614,9 +619,14 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
                                           const uint4 *__restrict__ w, const uint4 *__restrict__ wn, int lane,
                                           uint4 (&A)[DA][Plan<W, CT, NPT>::CTL],
                                           f32x4 (&acc)[Plan<W, CT, NPT>::n],
-                                          const int (&hoff)[Plan<W, CT, NPT>::NT]) {
+                                          const int (&hoff)[Plan<W, CT, NPT>::NT],
+                                          unsigned long long *kst = nullptr) {
     using PL = Plan<W, CT, NPT>;
     constexpr int NT = PL::NT, CTL = PL::CTL;
+    (void)kst;
+#ifdef SPAI_DIAG_KSTEP
+    if (kst) kst[20] = __builtin_amdgcn_s_memtime();   // stamp 44: conv start
+#endif
     static_assert(kKStepsRes % DA == 0, "the carried A ring needs DA | k-steps per layer");
     const int q = lane >> 4;
     f32x4 bv[CTL];
@@ -672,6 +682,9 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
             load_a(ks);
             final_tap_epilogue<W, CT, NPT, S, DA, DB, EPI, OUT>(smem, g, lane, A, B, bv, acc, hoff);
             load_a(ks + 1);
+#ifdef SPAI_DIAG_KSTEP
+            if (kst) kst[ks] = __builtin_amdgcn_s_memtime();
+#endif
             break;
         }
         load_a(ks);
@@ -709,6 +722,9 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
             }
         }
         __builtin_amdgcn_sched_barrier(0);
+#ifdef SPAI_DIAG_KSTEP
+        if (kst) kst[ks] = __builtin_amdgcn_s_memtime();
+#endif
     }
 }
 
@@ -1042,8 +1058,15 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
     for (int b = 0; b < P.blocks; ++b) {   // relu(x + BN(conv(relu(BN(conv(x)))))), model/mod.rs:152-165
         f32x4 acc[Plan<W, 4, NPT>::n];
         const int l1 = 2 * b, l2 = 2 * b + 1;
+        unsigned long long *kst = nullptr;
+#ifdef SPAI_DIAG_KSTEP
+        if (b == 1 && P.stamps && lane == 0) kst = P.stamps + ((size_t)blockIdx.x * kWaves + W) * kStamps + 24;
+#endif
         conv_mfma<W, 4, NPT, S, kX, DA, DB, 1, kY>(smem, g, bias + kHid * (1 + l1), P.w_res + l1 * kLayer,
-                                                                    P.w_res + l2 * kLayer, lane, A, acc, aux);
+                                                                    P.w_res + l2 * kLayer, lane, A, acc, aux, kst);
+#ifdef SPAI_DIAG_KSTEP
+        if (kst) kst[18] = __builtin_amdgcn_s_memtime();
+#endif
 #ifdef SPAI_DIAG
         if (b == 0 && !kDiagHead && !kDiagEntry) {   // make the k-loop's results visible before the stamp
             asm volatile("" ::"v"(acc[0][0]), "v"(acc[PL4::n - 1][3]));
@@ -1057,6 +1080,9 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
         }
 #endif
         layer_barrier();
+#ifdef SPAI_DIAG_KSTEP
+        if (kst) kst[19] = __builtin_amdgcn_s_memtime();
+#endif
 #ifdef SPAI_DIAG
         if (b == 0 && !kDiagHead && !kDiagEntry) stamp(P, W, lane, 19);
 #endif
@@ -1669,6 +1695,7 @@ int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
             const unsigned long long *sp = hs.data() + ((size_t)g * kWaves + w) * kStamps;
             if (!sp[0] || !sp[16]) continue;   // (a workgroup with no group)
             for (int k = 0; k < 20; ++k) cycles[k] += sp[k] ? (double)(long long)(sp[k] - sp[0]) : 0.0;
+            for (int k = 24; k < kStamps; ++k) cycles[k] += sp[k] ? (double)(long long)(sp[k] - sp[0]) : 0.0;
             cycles[20] += (double)(sp[0] - sp[20]);   // (the last group's stamp 0: one group per workgroup in the sweeps)
             cycles[21] += 10.0 * (double)(sp[22] - sp[21]);
             cycles[22] += 10.0 * (double)(sp[23] - sp[22]);
@@ -1676,7 +1703,8 @@ int net_phase_stamps(spai_net *n, uint32_t cnt, double *cycles) {
             last_out = std::max(last_out, sp[23]);
             cntw += 1;
         }
-    for (int k = 0; k < 23; ++k) cycles[k] /= cntw > 0 ? cntw : 1;
+    for (int k = 0; k < kStamps; ++k)
+        if (k != 23) cycles[k] /= cntw > 0 ? cntw : 1;
     cycles[23] = last_out > first_in ? 10.0 * (double)(last_out - first_in) : 0.0;
     return SPAI_OK;
 }

@@ -369,9 +369,11 @@ __global__ void k_troot_stats(TV T, const uint32_t *__restrict__ active, uint32_
     for (uint32_t k = 0; k < kCells; ++k) o[2 + k] = k < nch ? nodes[first + k].x : 0u;
 }
 
-__global__ void k_ttrees_init(TV T, uint32_t n) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
+// trees [0, n) -- or the n trees of `list` (streaming refills) -- become one-node trees at the empty board
+__global__ void k_ttrees_init(TV T, uint32_t n, const uint32_t *__restrict__ list) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t t = list ? list[i] : i;
     T.nodes[(size_t)t * T.cap] = make_uint4(0u, 0u, 0u, kNoChildren);
     T.root[t] = 0;
     T.next_free[t] = 1;
@@ -526,7 +528,7 @@ int trees_create(Engine *e, uint32_t n) {
         SPAI_TRY(e->blogits.alloc((size_t)n * 9));
         SPAI_TRY(e->bvalue.alloc(n));
     }
-    k_ttrees_init<<<(n + 63) / 64, 64, 0, e->stream>>>(view(e), n);
+    k_ttrees_init<<<(n + 63) / 64, 64, 0, e->stream>>>(view(e), n, nullptr);
     SPAI_HIP(hipGetLastError());
     SPAI_HIP(hipStreamSynchronize(e->stream));
     return SPAI_OK;
@@ -947,6 +949,7 @@ int ttt_selfplay(spai_ttt *e, uint32_t n_games, uint64_t gid_base, spai_sample_s
     };
     std::vector<std::vector<Rec>> hist(W);
     std::vector<uint32_t> act(W);
+    std::vector<uint32_t> refill;   // streaming: the slots reset at the end of a move
     std::vector<State> roots(W, State{0, 0, 0, 0});
     for (uint32_t i = 0; i < W; ++i) act[i] = i;
     double sims_done = 0, evals = 0, games = 0, positions = 0, moves = 0;
@@ -1012,16 +1015,23 @@ int ttt_selfplay(spai_ttt *e, uint32_t n_games, uint64_t gid_base, spai_sample_s
         std::vector<uint32_t> keep;
         for (uint32_t k = 0; k < na; ++k)
             if (!done[k]) keep.push_back(act[k]);
+        refill.clear();
         for (uint32_t k = 0; k < na && next_game < n_games; ++k)   // streaming: refill the ended games' slots
             if (done[k]) {
                 const uint32_t t = act[k];
                 slot_game[t] = next_game++;
                 slot_move[t] = 0;
                 roots[t] = State{0, 0, 0, 0};
-                k_ttree_reset<<<1, 1, 0, e->stream>>>(view(e), t, roots[t]);
-                SPAI_HIP(hipGetLastError());
+                refill.push_back(t);
                 keep.push_back(t);
             }
+        if (!refill.empty()) {   // one launch resets every refilled slot (stream order: before the next search's
+                                 // upload of the active list into the same buffer)
+            const uint32_t nr = (uint32_t)refill.size();
+            SPAI_HIP(hipMemcpyAsync(e->active.p, refill.data(), 4 * nr, hipMemcpyHostToDevice, e->stream));
+            k_ttrees_init<<<(nr + 255) / 256, 256, 0, e->stream>>>(view(e), nr, e->active.p);
+            SPAI_HIP(hipGetLastError());
+        }
         act.swap(keep);
     }
     if (stats) {

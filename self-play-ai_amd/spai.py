@@ -270,7 +270,7 @@ class Net:
         return lg, v
 
     def phase_cycles(self, count=4096):
-        c = np.zeros(24, np.float64)
+        c = np.zeros(48, np.float64)   # 24 stamps; 48 in the k-step diagnostic build (-DSPAI_DIAG_KSTEP)
         _check(lib().spai_net_phase_cycles(self.h, count, _p(c)))
         return c
 

@@ -1,11 +1,15 @@
 """The C ABI from a plain C99 client (tests/c/abi_client.c), compiled with gcc
 against include/spai.h and linked to libspai.so -- what a Rust/Go/JNI binding
 does.  CPU: it compiles with -Wall -Werror as C, links, and the host-only entry
-points answer.  GPU: a Connect4 search through the same client equals the
-oracle's visit counts (hash evaluator, bit-exact)."""
+points answer.  GPU, through include/spai.h alone: a Connect4 search equals the
+oracle's visit counts (hash evaluator, bit-exact); Model::predict (fp32 and bf16
+nets) against the libtorch golden and the fp32 oracle; self-play with a C sink
+callback bit-exact against the oracle's sample stream; an engine error code
+(SPAI_ERR_NAN) and recovery."""
 import os
 import subprocess
 
+import numpy as np
 import pytest
 
 from conftest import REPO
@@ -42,3 +46,84 @@ def test_c_client_search_matches_oracle(client, oracle):
         n = int(r[3])
         assert n == nc[t]
         assert [int(v) for v in r[5:5 + n]] == [int(v) for v in vis[t, :n]]
+
+
+def _hexf(s):
+    return np.float32(float.fromhex(s))
+
+
+@pytest.mark.gpu
+def test_c_client_predict_matches_golden_and_oracle(client, oracle, tmp_path):
+    """Model::predict through spai_net_create + spai_predict from C: the fp32 net on
+    the libtorch golden's boards within 1e-4 of libtorch and 2e-6 of the fp32
+    oracle (illegal columns exactly 0), the bf16 net within the bf16 tolerance"""
+    z = np.load(os.path.join(REPO, "tests", "golden", "net_c4_2x64.npz"))
+    blocks, params, b = int(z["meta"][0]), np.ascontiguousarray(z["params"], np.float32), z["boards"]
+    n = len(b)
+    params.tofile(tmp_path / "params.f32")
+    np.ascontiguousarray(b[:, :3], np.uint64).tofile(tmp_path / "boards.u64")
+    out = subprocess.run([client, "net", str(tmp_path / "params.f32"), str(params.size), str(blocks),
+                          str(tmp_path / "boards.u64"), str(n)], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    got = {"f32": np.zeros((n, 8), np.float32), "bf16": np.zeros((n, 8), np.float32)}
+    for l in out.stdout.splitlines():
+        if l.startswith("predict "):
+            f = l.split()
+            got[f[1]][int(f[2])] = [_hexf(v) for v in f[3:11]]
+    f32, bf = got["f32"], got["bf16"]
+    np.testing.assert_allclose(f32[:, 1:], z["priors"], rtol=1e-4, atol=1e-5)
+    on = oracle.Net(oracle.GAME_CONNECT4, blocks, 64, params)
+    from test_gpu_parity import _oracle_state
+    sts = [_oracle_state(oracle, int(b[i, 0]), int(b[i, 1]), int(b[i, 2]), 0) for i in range(n)]
+    arr = (oracle.C.c_void_p * n)(*[oracle.C.addressof(s.st) for s in sts])
+    rp, rv = np.zeros((n, 7), np.float32), np.zeros(n, np.float32)
+    oracle.lib().or_predict(on.h, n, arr, oracle._f(rp), oracle._f(rv))
+    np.testing.assert_allclose(f32[:, 1:], rp, rtol=2e-6, atol=2e-7)
+    np.testing.assert_allclose(f32[:, 0], rv, rtol=1e-6, atol=2e-7)
+    assert np.all((f32[:, 1:] == 0) == (rp == 0)) and np.all((bf[:, 1:] == 0) == (rp == 0))
+    np.testing.assert_allclose(bf[:, 1:], rp, atol=2e-2)
+    np.testing.assert_allclose(bf[:, 0], rv, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.gpu
+def test_c_client_selfplay_sink_matches_oracle(client, oracle):
+    """SelfPlayWorker::self_play through spai_selfplay_run with a C sink callback
+    (hash evaluator): every game's moves, and per position the value, the visit
+    policy and the encoding, bit-exact against the oracle in its emission order"""
+    games, sims, seed = 24, 32, 5
+    out = subprocess.run([client, "selfplay", str(games), str(sims), str(seed)], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr
+    ref = oracle.self_play(oracle.GAME_CONNECT4, games, sims, seed, eval_kind=oracle.EVAL_HASH, max_plies=42)
+    k, gid, seen = 0, None, 0
+    for l in out.stdout.splitlines():
+        f = l.split()
+        if f[0] == "game":
+            gid, m = int(f[1]), int(f[2])
+            assert [int(v) for v in f[3:3 + m]] == list(ref["moves"][gid, :m])
+            seen += 1
+        elif f[0] == "pos":
+            assert ref["game"][k] == gid
+            assert _hexf(f[1]) == ref["value"][k]
+            bits = int(f[2], 16) | (int(f[3], 16) << 64)
+            enc = np.array([(bits >> i) & 1 for i in range(126)], np.float32)
+            np.testing.assert_array_equal(enc, ref["enc"][k])
+            np.testing.assert_array_equal(np.array([_hexf(v) for v in f[4:11]]), ref["policy"][k])
+            k += 1
+        elif f[0] == "stats":
+            assert int(f[1]) == games and float(f[2]) == games and float(f[3]) == ref["sims"]
+            assert float(f[4]) == k
+    assert seen == games and k == len(ref["value"])
+
+
+@pytest.mark.gpu
+def test_c_client_engine_error_path(client):
+    """an engine error crosses the C boundary as a code and a message: a NaN value
+    bias makes spai_search return SPAI_ERR_NAN (-5; the reference panics,
+    mcts.rs:106-109), and the engine then searches normally with a clean net"""
+    out = subprocess.run([client, "nan"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    lines = {l.split(" ", 1)[0]: l.split(" ", 1)[1] for l in out.stdout.strip().splitlines() if " " in l}
+    rc, msg = lines["nan_rc"].split(" ", 1)
+    assert int(rc) == -5 and "nan" in msg.lower(), lines["nan_rc"]
+    assert int(lines["recovered"]) == 64 * 7   # 8 sims: the first expands the root, 7 visit its children
