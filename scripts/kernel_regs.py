@@ -14,8 +14,9 @@ import tempfile
 B = "/opt/rocm/lib/llvm/bin"
 
 
-def main():
-    path, rx = sys.argv[1], re.compile(sys.argv[2] if len(sys.argv) > 2 else ".")
+def kernels(path):
+    """{kernel name: descriptor fields} of every gfx950 kernel in a built library"""
+    out = {}
     with tempfile.TemporaryDirectory() as t:
         fb = os.path.join(t, "fb.bin")
         subprocess.run([f"{B}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", path, os.path.join(t, "s")], check=True)
@@ -33,10 +34,18 @@ def main():
             notes = subprocess.run([f"{B}/llvm-readelf", "--notes", co], capture_output=True, text=True).stdout
             for ent in notes.split("  - .agpr_count:")[1:]:
                 f = dict(re.findall(r"\.(\w+):\s+(\S+)", ent))
-                name = f.get("name", "?")
-                if rx.search(name):
-                    print(f"{name[:70]:70s} vgpr {f.get('vgpr_count')} (agpr {ent.split()[0]}) sgpr {f.get('sgpr_count')} "
-                          f"vspill {f.get('vgpr_spill_count')} lds {f.get('group_segment_fixed_size')}")
+                f["agpr_count"] = ent.split()[0]
+                out[f.get("name", "?")] = f
+    return out
+
+
+def main():
+    path, rx = sys.argv[1], re.compile(sys.argv[2] if len(sys.argv) > 2 else ".")
+    for name, f in kernels(path).items():
+        if rx.search(name):
+            print(f"{name[:70]:70s} vgpr {f.get('vgpr_count')} (agpr {f['agpr_count']}) sgpr {f.get('sgpr_count')} "
+                  f"vspill {f.get('vgpr_spill_count')} scratch {f.get('private_segment_fixed_size')} "
+                  f"lds {f.get('group_segment_fixed_size')}")
 
 
 if __name__ == "__main__":

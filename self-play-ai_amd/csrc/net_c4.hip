@@ -262,6 +262,23 @@ __host__ __device__ constexpr int first_kstep(int S, int t) {
 #ifndef SPAI_HEAD_CO_MAJOR_MAX_NPT
 #define SPAI_HEAD_CO_MAJOR_MAX_NPT 8   // the head conv (CT = 3) in co-major order up to this many tiles
 #endif
+// Deferred epilogue (SPAI_DEFER_EPI).  A trunk conv's fused epilogue (ReLU, bf16 pack,
+// LDS store: 8 VALU + a store per task) cannot hide in the last tap's MFMA gaps (an
+// MFMA leaves 8 issue cycles free, a task's epilogue needs ~44), so at the
+// position-major group sizes (S >= 5) the tasks of co tiles 2 and 3 -- output
+// channels 32-63 -- keep their fp32 accumulators into the NEXT layer, which runs the
+// K-half-0 k-steps of every tap (input channels 0-31) first and does those deferred
+// epilogues in their MFMA gaps; a barrier then publishes channels 32-63 before the
+// K-half-1 k-steps read them.  The K order is the same at every group size (the sums,
+// and so the results, do not depend on S).
+#ifdef SPAI_DEFER_EPI
+constexpr bool kDefer = true;
+#else
+constexpr bool kDefer = false;
+#endif
+// k-step executed j-th in a layer (k = tap * 2 + K half)
+__host__ __device__ constexpr int kstep_of(int j) { return kDefer ? (j < 9 ? 2 * j : 2 * (j - 9) + 1) : j; }
+
 template <int W, int CT, int NPT>
 struct Plan {
     static constexpr int MODE = NPT <= (CT == 3 ? SPAI_HEAD_CO_MAJOR_MAX_NPT : SPAI_CO_MAJOR_MAX_NPT) ? 1
@@ -290,6 +307,19 @@ struct Plan {
         return MODE == 2 ? (i < 2 * m ? 2 * pj + (i & 1) : 2 * pj + ph)
                          : MODE == 1 ? (first + i) / NPT : (first + i) % CT;
     }
+    // deferred epilogue: the position-major 64-channel plans defer their co-tile 2/3 tasks
+    static constexpr bool DEFER = kDefer && CT == 4 && MODE == 0;
+    static constexpr int count_deferred() {
+        int c = 0;
+        for (int i = 0; i < n; ++i) c += co(i) >= 2;
+        return c;
+    }
+    static constexpr int ND = DEFER ? count_deferred() : 0;
+    // the deferred accumulators are indexed by task (dacc[i], only the deferred ones live):
+    // every index stays a plain expression of the unrolled loop counters, so the arrays are
+    // scalarised into registers (a loop-valued task map left them on the scratch stack)
+    static constexpr int NDA = ND > 0 ? n : 1;
+    static constexpr bool deferred(int i) { return DEFER && co(i) >= 2; }
 };
 
 // Per-lane LDS geometry, computed once per kernel (positions are the same for
@@ -519,9 +549,16 @@ __device__ __forceinline__ void final_tap_epilogue(uint8_t *smem, const Geo<Plan
                                                    const uint4 (&B)[DB][Plan<W, CT, NPT>::NT],
                                                    const f32x4 (&bv)[Plan<W, CT, NPT>::CTL],
                                                    f32x4 (&acc)[Plan<W, CT, NPT>::n],
-                                                   const int (&hoff)[Plan<W, CT, NPT>::NT]) {
+                                                   const int (&hoff)[Plan<W, CT, NPT>::NT],
+                                                   f32x4 (&dacc)[Plan<W, CT, NPT>::NDA]) {
     using PL = Plan<W, CT, NPT>;
+    // (EPI 1/2 with a deferring plan: the co-tile 2/3 tasks hand their accumulators on instead)
+    auto defer = [](int i) { return EPI < 3 && PL::deferred(i); };
+#ifdef SPAI_EXP_EPI_LAG
+    constexpr int n = PL::n, k0 = kKStepsRes - 2, D = SPAI_EXP_EPI_LAG;   // timing experiment: epilogue lag
+#else
     constexpr int n = PL::n, k0 = kKStepsRes - 2, D = 2;
+#endif
     static_assert(CT == 4, "fused epilogue: 64-channel layers");
     auto live = [](int t, int ks) { return !((tap_skip(S, PL::gpt(t)) >> (ks >> 1)) & 1); };
     auto task_on = [](int i) { return !(EPI == 3 && PL::co(i) == 3); };   // the head has no co tile 3
@@ -557,25 +594,38 @@ __device__ __forceinline__ void final_tap_epilogue(uint8_t *smem, const Geo<Plan
             }
             const int t = PL::gpt(PL::pt(i)), c = PL::co(i) - PL::C0;
 #pragma unroll
-            for (int ks = k0; ks < kKStepsRes; ++ks)
+            for (int j = k0; j < kKStepsRes; ++j) {
+                const int ks = kstep_of(j);
                 if (task_on(i) && live(PL::pt(i), ks)) {
-                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[ks % DA][c]), as_bf16x8(B[ks % DB][PL::pt(i)]),
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[j % DA][c]), as_bf16x8(B[j % DB][PL::pt(i)]),
                                                                     ks == first_kstep(S, t) ? bv[c] : acc[i], 0, 0, 0);
                     ++nm;
                 }
+            }
             if (EPI == 2) {
                 acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(id[PL::co(i) & 1]), as_bf16x8(rb[i % 3]), acc[i],
                                                                 0, 0, 0);
                 ++nm;
             }
         }
-        if (i >= D && EPI < 3) {
+        if (i >= D && EPI < 3 && !defer(i - D)) {
             const int j = i - D;
             const int off = OUT + (g.epi[PL::pt(j)] ^ (PL::co(j) << 5));
+#if defined(SPAI_EXP_NOEPI) || defined(SPAI_EXP_NOEPI_ALL)
+            // timing-only deletion experiments (wrong results): no conversion VALU (the accumulator
+            // kept alive in its AGPRs), zeros stored -- or (NOEPI_ALL) no store either
+            asm volatile("" ::"a"(acc[j]));
+#ifdef SPAI_EXP_NOEPI
+            *(uint2 *)(smem + off) = make_uint2(0u, (uint32_t)off);
+            nw = 1;
+#endif
+            nv = 0;
+#else
             *(uint2 *)(smem + off) = make_uint2(pack_relu_bf16x2(acc[j][0], acc[j][1]), pack_relu_bf16x2(acc[j][2], acc[j][3]));
             nv = 5;
             nw = 1;
-        } else if (i >= D && task_on(i - D)) {   // the head: H[s][cell * 36 + c] for the 35 real channels
+#endif
+        } else if (EPI == 3 && i >= D && task_on(i - D)) {   // the head: H[s][cell * 36 + c] for the 35 real channels
             const int j = i - D, co0 = PL::co(j) * 16 + 4 * (lane >> 4), off = hoff[PL::pt(j)];
             // a lane with nothing to store writes its own word of the (not yet used) linear partials
             const int addr = co0 < kHC && off >= 0 ? kH + 2 * (off + co0) : kL + 8 * lane;
@@ -605,6 +655,11 @@ __device__ __forceinline__ void final_tap_epilogue(uint8_t *smem, const Geo<Plan
         if (nrd) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (EPI < 3 && PL::ND > 0) {
+#pragma unroll
+        for (int i = 0; i < PL::n; ++i)
+            if (PL::deferred(i)) dacc[i] = acc[i];
+    }
 }
 
 // EPI > 0 fuses the layer's epilogue into its last tap (k-steps 16 and 17): the
@@ -620,6 +675,7 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
                                           uint4 (&A)[DA][Plan<W, CT, NPT>::CTL],
                                           f32x4 (&acc)[Plan<W, CT, NPT>::n],
                                           const int (&hoff)[Plan<W, CT, NPT>::NT],
+                                          f32x4 (&dacc)[Plan<W, CT, NPT>::NDA],
                                           unsigned long long *kst = nullptr) {
     using PL = Plan<W, CT, NPT>;
     constexpr int NT = PL::NT, CTL = PL::CTL;
@@ -648,6 +704,7 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
         return on;
     };
     auto live = [&](int t, int ks) { return tile_on(t) && !((tap_skip(S, PL::gpt(t)) >> (ks >> 1)) & 1); };
+#ifndef SPAI_DEFER_EPI   // the k-loop in k-step order (production)
     uint4 B[DB][NT];
 #pragma unroll
     for (int kb = 0; kb < DB - 1; ++kb) {
@@ -680,7 +737,7 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
                     if (live(t, ks + lb)) B[(ks + lb) % DB][t] = *(const uint4 *)(smem + (IN - 256) + (g.b(t, tap) ^ flip));
             }
             load_a(ks);
-            final_tap_epilogue<W, CT, NPT, S, DA, DB, EPI, OUT>(smem, g, lane, A, B, bv, acc, hoff);
+            final_tap_epilogue<W, CT, NPT, S, DA, DB, EPI, OUT>(smem, g, lane, A, B, bv, acc, hoff, dacc);
             load_a(ks + 1);
 #ifdef SPAI_DIAG_KSTEP
             if (kst) kst[ks] = __builtin_amdgcn_s_memtime();
@@ -726,6 +783,104 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
         if (kst) kst[ks] = __builtin_amdgcn_s_memtime();
 #endif
     }
+#else   // SPAI_DEFER_EPI: K-half-0 k-steps first, the previous layer's deferred epilogue in their gaps
+    uint4 B[DB][NT];
+    // B fragments of the j-th executed k-step (its tap and K half)
+    auto read_b = [&](int j) {
+        const int ks = kstep_of(j), tap = ks >> 1, flip = (ks & 1) << 6;
+        int nr = 0;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+            if (live(t, ks)) {
+                B[j % DB][t] = exp_b(smem + (IN - 256) + (g.b(t, tap) ^ flip), lane, j + t);
+                ++nr;
+            }
+        return nr;
+    };
+#pragma unroll
+    for (int kb = 0; kb < DB - 1; ++kb) read_b(kb);
+    constexpr int la = DA - 1, lb = DB - 1;
+    // A for the k-step executed (j + la)-th (this layer's, or the next layer's first ones)
+    auto load_a = [&](int j) {
+        if (j + la < kKStepsRes) {
+            const int ks = kstep_of(j + la);
+#pragma unroll
+            for (int c = 0; c < CTL; ++c)
+                if (!(EPI == 3 && PL::C0 + c == 3)) A[(j + la) % DA][c] = exp_a(wl[(ks * CT + c) * 64], lane, j + c);
+        } else if (EPI != 3) {   // (nothing follows the head)
+            const int ks = kstep_of(j + la - kKStepsRes);
+#pragma unroll
+            for (int c = 0; c < CTL; ++c) A[(j + la) % DA][c] = exp_a(wnl[(ks * CT + c) * 64], lane, j + c);
+        }
+    };
+    // deferred epilogue of the previous layer (its co-tile 2/3 tasks, output channels
+    // 32-63 of IN) in the MFMA gaps of the K-half-0 k-steps; the barrier at the top of
+    // step jb publishes them before the first K-half-1 B reads (issued lb steps ahead)
+    constexpr int jb = 9 - lb;
+    constexpr bool din = PL::ND > 0;
+#pragma unroll
+    for (int j = 0; j < kKStepsRes; ++j) {
+        const int ks = kstep_of(j);
+        if constexpr (din) if (j == jb) __syncthreads();
+        if constexpr (EPI > 0) if (j == kKStepsRes - 2) {
+            // B reads of the last k-step (if not issued yet), then the fused final tap;
+            // the last k-step's A prefetch waits for the MFMAs that read the slot it refills
+            if (j + lb < kKStepsRes) read_b(j + lb);
+            load_a(j);
+            final_tap_epilogue<W, CT, NPT, S, DA, DB, EPI, OUT>(smem, g, lane, A, B, bv, acc, hoff, dacc);
+            load_a(j + 1);
+#ifdef SPAI_DIAG_KSTEP
+            if (kst) kst[j] = __builtin_amdgcn_s_memtime();
+#endif
+            break;
+        }
+        load_a(j);
+        const int nr = j + lb < kKStepsRes ? read_b(j + lb) : 0;   // B reads issued this k-step (issue hints)
+        int nm = 0;
+#pragma unroll
+        for (int i = 0; i < PL::n; ++i)
+            if (task_on(i) && live(PL::pt(i), ks)) {
+                const int t = PL::gpt(PL::pt(i));
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[j % DA][PL::co(i) - PL::C0]),
+                                                                as_bf16x8(B[j % DB][PL::pt(i)]),
+                                                                ks == first_kstep(S, t) ? bv[PL::co(i) - PL::C0]
+                                                                                        : acc[i], 0, 0, 0);
+                ++nm;
+            }
+        int ndw = 0;   // deferred epilogue tasks stored this k-step (tasks [j n / jb, (j + 1) n / jb))
+        if constexpr (din) {
+#pragma unroll
+            for (int i = 0; i < PL::n; ++i)
+                if (j < jb && i >= j * PL::n / jb && i < (j + 1) * PL::n / jb && PL::deferred(i)) {
+                    const int off = IN + (g.epi[PL::pt(i)] ^ (PL::co(i) << 5));
+                    *(uint2 *)(smem + off) = make_uint2(pack_relu_bf16x2(dacc[i][0], dacc[i][1]),
+                                                        pack_relu_bf16x2(dacc[i][2], dacc[i][3]));
+                    ++ndw;
+                }
+        }
+        // issue order for this k-step: each MFMA followed by up to 2 VALU, one
+        // LDS read (next B) and one weight load (A, DA-1 ahead); deferred stores last
+        const int ng = nm > nr ? nm : nr;
+#pragma unroll
+        for (int i = 0; i < PL::n; ++i) {
+            if (i < ng) {
+                if (i < nm) __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                if (i < nr) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                if (i < CTL) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
+        }
+        if constexpr (din) {
+#pragma unroll
+            for (int k = 0; k < PL::n; ++k)
+                if (k < ndw) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#ifdef SPAI_DIAG_KSTEP
+        if (kst) kst[j] = __builtin_amdgcn_s_memtime();
+#endif
+    }
+#endif
 }
 
 template <int CT, int C0, int CTL, int DA>
@@ -733,16 +888,21 @@ __device__ __forceinline__ void load_a_first(const uint4 *__restrict__ w, int la
 #pragma unroll
     for (int k = 0; k < DA - 1; ++k)
 #pragma unroll
-        for (int c = 0; c < CTL; ++c) A[k][c] = w[(k * CT + C0 + c) * 64 + lane];
+        for (int c = 0; c < CTL; ++c) A[k][c] = w[(kstep_of(k) * CT + C0 + c) * 64 + lane];
 }
 
 // epilogue for a 64-channel bf16 output: relu(acc) -> LDS at OUT (the stem's;
 // the trunk and head convs fuse theirs into the last tap, final_tap_epilogue)
 template <int W, int NPT, int OUT>
-__device__ __forceinline__ void epilogue_act(uint8_t *smem, const Geo<Plan<W, 4, NPT>::NT> &g, f32x4 (&acc)[Plan<W, 4, NPT>::n]) {
+__device__ __forceinline__ void epilogue_act(uint8_t *smem, const Geo<Plan<W, 4, NPT>::NT> &g, f32x4 (&acc)[Plan<W, 4, NPT>::n],
+                                             f32x4 (&dacc)[Plan<W, 4, NPT>::NDA]) {
     using PL = Plan<W, 4, NPT>;
 #pragma unroll
     for (int i = 0; i < PL::n; ++i) {
+        if (PL::deferred(i)) {   // stored by the first trunk conv's K-half-0 k-steps
+            dacc[i] = acc[i];
+            continue;
+        }
         const int off = OUT + (g.epi[PL::pt(i)] ^ (PL::co(i) << 5));
         *(uint2 *)(smem + off) = make_uint2(pack_relu_bf16x2(acc[i][0], acc[i][1]), pack_relu_bf16x2(acc[i][2], acc[i][3]));
     }
@@ -756,7 +916,8 @@ __device__ __forceinline__ void epilogue_act(uint8_t *smem, const Geo<Plan<W, 4,
 template <int W, int S, bool FROM_X>
 __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const float *__restrict__ x, int base_slot,
                                      int valid, int lane, const Geo<Plan<W, 4, npt_of(S)>::NT> &g,
-                                     const int (&aux)[Plan<W, 4, npt_of(S)>::NT]) {
+                                     const int (&aux)[Plan<W, 4, npt_of(S)>::NT],
+                                     f32x4 (&dacc)[Plan<W, 4, npt_of(S)>::NDA]) {
     constexpr int NPT = npt_of(S);
     using PL = Plan<W, 4, NPT>;
     constexpr int NT = PL::NT;
@@ -808,7 +969,7 @@ __device__ __forceinline__ void stem(uint8_t *smem, const NetParams &P, const fl
     for (int i = 0; i < PL::n; ++i)
         acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(a[PL::co(i)]), as_bf16x8(bv[PL::pt(i)]),
                                                         b4[PL::co(i)], 0, 0, 0);
-    epilogue_act<W, NPT, kX>(smem, g, acc);
+    epilogue_act<W, NPT, kX>(smem, g, acc, dacc);
 }
 
 // The head conv (64 -> 32 policy + 3 value channels) on the 64-channel layers'
@@ -820,7 +981,8 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
                                            const Geo<Plan<W, 4, npt_of(S)>::NT> &g,
                                            const int (&aux)[Plan<W, 4, npt_of(S)>::NT],
                                            uint4 (&A)[DA][Plan<W, 4, npt_of(S)>::CTL],
-                                           uint4 (&wlin)[kLinWPer]) {
+                                           uint4 (&wlin)[kLinWPer],
+                                           f32x4 (&dacc)[Plan<W, 4, npt_of(S)>::NDA]) {
     constexpr int NPT = npt_of(S);
     using PL = Plan<W, 4, NPT>;
     int hoff[PL::NT];   // head-feature offset of each tile's row (-1: padding)
@@ -833,7 +995,7 @@ __device__ __forceinline__ void head_layer(uint8_t *smem, const NetParams &P, in
     for (int i = 0; i < kLinWPer; ++i) wlin[i] = P.w_lin[(W * kLinWPer + i) * 64 + lane];   // consumed after the head conv
     f32x4 acc[PL::n];
     conv_mfma<W, 4, NPT, S, kX, DA, b_depth(S), 3, kH>(smem, g, (const float *)(smem + kBias) + kHid * (1 + 2 * P.blocks),
-                                                      P.w_head, P.w_head, lane, A, acc, hoff);
+                                                      P.w_head, P.w_head, lane, A, acc, hoff, dacc);
 #ifdef SPAI_DIAG
     if (kDiagHead) stamp(P, W, lane, 17);
 #endif
@@ -1018,7 +1180,9 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
         constexpr int DA = 3, DB = b_depth(S), SW = KH == 2 ? -1 : W;
         uint4 A[DA][PL4::CTL];
         if (P.blocks > 0) load_a_first_split<KH, PL4::CTL, PL4::C0, DA>(P.w_res, lane, A);
-        if (KH == 1) stem<W, S, FROM_X>(smem, P, x, base, valid, lane, g, aux);
+        static_assert(!kDefer, "SPAI_W8 has no deferred epilogue");
+        f32x4 dacc[PL4::NDA];
+        if (KH == 1) stem<W, S, FROM_X>(smem, P, x, base, valid, lane, g, aux, dacc);
         __syncthreads();
         stamp(P, SW, lane, 1);
         for (int b = 0; b < P.blocks; ++b) {
@@ -1039,7 +1203,7 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
             constexpr int DH = a_depth(S);
             uint4 Ah[DH][PL4::CTL];
             load_a_first<4, PL4::C0, PL4::CTL, DH>(P.w_head, lane, Ah);
-            head_layer<W, S, DH>(smem, P, lane, g, aux, Ah, wlin);
+            head_layer<W, S, DH>(smem, P, lane, g, aux, Ah, wlin, dacc);
         }
         __syncthreads();
         stamp(P, SW, lane, 14);
@@ -1049,7 +1213,8 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
     constexpr int DA = a_depth(S), DB = b_depth(S);
     uint4 A[DA][PL4::CTL];
     load_a_first<4, PL4::C0, PL4::CTL, DA>(P.blocks > 0 ? P.w_res : P.w_head, lane, A);
-    stem<W, S, FROM_X>(smem, P, x, base, valid, lane, g, aux);
+    f32x4 dacc[PL4::NDA];   // deferred epilogue accumulators, handed from each layer to the next
+    stem<W, S, FROM_X>(smem, P, x, base, valid, lane, g, aux, dacc);
     __syncthreads();
     stamp(P, W, lane, 1);
 #ifdef SPAI_C4_BLOCK_UNROLL
@@ -1063,7 +1228,7 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
         if (b == 1 && P.stamps && lane == 0) kst = P.stamps + ((size_t)blockIdx.x * kWaves + W) * kStamps + 24;
 #endif
         conv_mfma<W, 4, NPT, S, kX, DA, DB, 1, kY>(smem, g, bias + kHid * (1 + l1), P.w_res + l1 * kLayer,
-                                                                    P.w_res + l2 * kLayer, lane, A, acc, aux, kst);
+                                                                    P.w_res + l2 * kLayer, lane, A, acc, aux, dacc, kst);
 #ifdef SPAI_DIAG_KSTEP
         if (kst) kst[18] = __builtin_amdgcn_s_memtime();
 #endif
@@ -1088,13 +1253,13 @@ __device__ __forceinline__ void torso_and_heads(uint8_t *smem, const NetParams &
 #endif
         if (l1 < 12) stamp(P, W, lane, 2 + l1);
         conv_mfma<W, 4, NPT, S, kY, DA, DB, 2, kX>(smem, g, bias + kHid * (1 + l2), P.w_res + l2 * kLayer,
-                            b + 1 < P.blocks ? P.w_res + (l2 + 1) * kLayer : P.w_head, lane, A, acc, aux);
+                            b + 1 < P.blocks ? P.w_res + (l2 + 1) * kLayer : P.w_head, lane, A, acc, aux, dacc);
         layer_barrier();
         if (l2 < 12) stamp(P, W, lane, 2 + l2);
     }
     if (kDiagHead) stamp(P, W, lane, 19);   // diagnostic head mode: 19 = before the head, 17 = head k-loop, 18 = H written
     uint4 wlin[kLinWPer];
-    head_layer<W, S, DA>(smem, P, lane, g, aux, A, wlin);
+    head_layer<W, S, DA>(smem, P, lane, g, aux, A, wlin, dacc);
     __syncthreads();
     stamp(P, W, lane, 14);
     linear_mfma<W, S>(smem, lane, wlin);
