@@ -147,3 +147,46 @@ def test_stream_game_ids_partition(world):
     assert sorted(warm) == list(range(-w * world * G, 0))
     if world == 1:
         assert timed == [g for i in range(k) for g in range(i * G, (i + 1) * G)]
+
+
+_RCCL_FAIL = r"""
+import sys
+sys.path.insert(0, {repo!r})
+import bench
+
+class G:
+    def allgather(self, x):
+        return [0, 1] if isinstance(x, int) else [x, x]
+    def broadcast_bytes(self, b):
+        return b or bytes(128)
+
+class D:
+    world, rank, local = {world}, 0, 0
+    g = G()
+
+class S:
+    @staticmethod
+    def comm_unique_id():
+        return bytes(128)
+    class Comm:
+        def __init__(self, *a):
+            raise RuntimeError("ncclCommInitRank failed (simulated)")
+
+comm, note = bench.rccl_comm(D(), S)
+print("returned", comm, note)
+"""
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_rccl_failure_stops_the_rank(tmp_path, world):
+    """at world > 1 a rank whose RCCL communicator fails exits at once with a
+    non-zero status (its peers may sit inside ncclCommInitRank, which has no timeout,
+    so spawn_ranks or the launcher must stop them); at world 1 the failure is only
+    reported in the line"""
+    p = subprocess.run([sys.executable, "-c", _RCCL_FAIL.format(repo=REPO, world=world)], capture_output=True,
+                       text=True, timeout=60)
+    if world == 1:
+        assert p.returncode == 0 and "returned None RCCL communicator failed" in p.stdout, (p.stdout, p.stderr)
+    else:
+        assert p.returncode == 3 and "returned" not in p.stdout, (p.returncode, p.stdout)
+        assert "RCCL communicator failed on rank 0" in p.stderr

@@ -194,3 +194,15 @@ def test_bench_gpus_flag_spawns_ranks():
         assert two["work"][k] == one["work"][k], (k, one["work"], two["work"])
     assert one["rccl_ranks"] == 1 and one["rccl"]["counters_agree"] is True, one["rccl"]
     assert two["rccl_ranks"] == 0 and "share" in two["rccl"]["note"], two["rccl"]
+    # per-rank balance and the host-core budget: every rank reports its
+    # own simulations, wall time and host CPU seconds; the ranks' work sums to the line's
+    for line, world in ((one, 1), (two, 2)):
+        pr = line["per_rank"]
+        assert sorted(r["rank"] for r in pr) == list(range(world))
+        assert sum(r["sims"] for r in pr) == line["work"]["sims"]
+        assert sum(r["games"] for r in pr) == line["work"]["games"]
+        for r in pr:
+            assert r["wall_s"] > 0 and r["host_cpu_s"] > 0 and r["sims_per_sec"] > 0
+            assert abs(r["host_cpu_share"] - r["host_cpu_s"] / r["wall_s"]) < 1e-9
+        assert line["host"]["cpu_share_per_rank_max"] == max(r["host_cpu_share"] for r in pr)
+        assert line["schedule"] == "streamed"
