@@ -140,6 +140,15 @@ int spai_engine_create(int game, const spai_config *cfg, int device, spai_engine
     SPAI_HIP(hipGetDeviceCount(&ndev));
     SPAI_CHECK(device >= 0 && device < ndev, SPAI_ERR_DEVICE, "device %d not present (%d visible)", device, ndev);
     SPAI_HIP(hipSetDevice(device));
+    // SPAI_BLOCKING_SYNC=1 (A/B knob): host waits on the device sleep instead of spinning,
+    // so a rank's self-play host loop needs less than a core beside its GPU (DESIGN.md §6:
+    // the host-core budget of an 8-GPU node).  Takes effect only before the device's
+    // first use in the process.
+    static const bool blocking_sync = [] {
+        const char *v = std::getenv("SPAI_BLOCKING_SYNC");
+        return v && std::atoi(v) != 0;
+    }();
+    if (blocking_sync) (void)hipSetDeviceFlags(hipDeviceScheduleBlockingSync);
     spai_engine *e = new (std::nothrow) spai_engine();
     SPAI_CHECK(e, SPAI_ERR_INVALID, "out of host memory");
     e->game = game;
