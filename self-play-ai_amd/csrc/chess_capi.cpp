@@ -116,7 +116,7 @@ int spai_chess_create(const spai_config *cfg, int device, spai_chess **out) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess) e->n_cu = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess || e->err.alloc(1) != SPAI_OK ||
-        hipMemset(e->err.p, 0, 4) != hipSuccess) {
+        hipMemsetAsync(e->err.p, 0, 4, e->stream) != hipSuccess) {
         set_error("chess engine stream / scratch allocation failed");
         delete e;
         return SPAI_ERR_DEVICE;

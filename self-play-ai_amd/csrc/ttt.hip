@@ -486,7 +486,7 @@ int run_search(Engine *e, uint32_t na, uint32_t sims) {
     SPAI_HIP(hipMemcpyAsync(&f, e->err.p, 4, hipMemcpyDeviceToHost, e->stream));
     SPAI_HIP(hipStreamSynchronize(e->stream));
     if (f) {
-        SPAI_HIP(hipMemset(e->err.p, 0, 4));
+        SPAI_HIP(hipMemsetAsync(e->err.p, 0, 4, e->stream));   // stream-ordered (the stream is non-blocking)
         if (f & kErrNan) {
             set_error("NaN UCB score (the reference panics, mcts.rs:106-109)");
             return SPAI_ERR_NAN;
@@ -621,7 +621,7 @@ int spai_ttt_create(const spai_config *cfg, int device, spai_ttt **out) {
     e->device = device;
     e->cfg = *cfg;
     if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess || e->err.alloc(1) != SPAI_OK ||
-        hipMemset(e->err.p, 0, 4) != hipSuccess) {
+        hipMemsetAsync(e->err.p, 0, 4, e->stream) != hipSuccess) {
         set_error("ttt engine stream / scratch allocation failed");
         delete e;
         return SPAI_ERR_DEVICE;
@@ -655,7 +655,10 @@ int spai_ttt_games_resize(spai_ttt *e, uint32_t n) {
     SPAI_TRY(e->sf2.alloc((size_t)n * 9));
     e->n_slots = n;
     if (n) {
-        SPAI_HIP(hipMemset(e->slots.p, 0, sizeof(State) * n));
+        // on the engine's (non-blocking) stream: a plain hipMemset is not ordered before the
+        // rules kernels that stream launches next, and one GPU run read the slots unzeroed
+        SPAI_HIP(hipMemsetAsync(e->slots.p, 0, sizeof(State) * n, e->stream));
+        SPAI_HIP(hipStreamSynchronize(e->stream));
     }
     return SPAI_OK;
 }
