@@ -8,6 +8,7 @@
 //                 counter and a generation word, agent-scope release/acquire, the
 //                 arriving workgroup's thread 0 spins (s_sleep) on the generation;
 //                 reported: wall time per barrier (HIP events over the launch)
+//   mode barrier2: the same with a two-level barrier (8 group counters, then one)
 //   mode chain:   N launches of the same G-workgroup kernel doing nothing but its
 //                 entry/exit, back to back on one stream: wall time per launch
 //   mode chain_work: as chain, each launch touching 64 KiB (a BN-sized pass)
@@ -53,6 +54,48 @@ __device__ __forceinline__ bool grid_barrier(unsigned *count, unsigned G) {
     return ok;
 }
 
+// two-level: the workgroups of group b % 8 (one group per XCD when the dispatcher
+// places workgroups round-robin, as MI355X does; correct for any placement) arrive on
+// their group's counter (own 128-B line); each group's last arrival arrives on the
+// global counter, whose last arrival bumps the generation.  c[32 g] = group g,
+// c[256] = global, c[288] = generation.
+__device__ __forceinline__ bool grid_barrier2(unsigned *c, unsigned G) {
+    __syncthreads();
+    bool ok = true;
+    if (threadIdx.x == 0) {
+        const unsigned grp = blockIdx.x % 8, gsize = G / 8 + (grp < G % 8 ? 1u : 0u), ngroups = G < 8 ? G : 8;
+        const unsigned g = __hip_atomic_load(c + 288, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool last = false;
+        if (__hip_atomic_fetch_add(c + 32 * grp, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+            __hip_atomic_store(c + 32 * grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = __hip_atomic_fetch_add(c + 256, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1;
+        }
+        if (last) {
+            __hip_atomic_store(c + 256, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(c + 288, g + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            unsigned spins = 0;
+            while (__hip_atomic_load(c + 288, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1u << 24)) {
+                    ok = false;
+                    break;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    return ok;
+}
+
+__global__ __launch_bounds__(256) void k_barriers2(unsigned *c, unsigned G, int n, unsigned *fail) {
+    for (int i = 0; i < n; ++i)
+        if (!grid_barrier2(c, G)) {
+            if (threadIdx.x == 0) atomicAdd(fail, 1u);
+            return;
+        }
+}
+
 __global__ __launch_bounds__(256) void k_barriers(unsigned *count, unsigned G, int n, unsigned *fail) {
     for (int i = 0; i < n; ++i)
         if (!grid_barrier(count, G)) {
@@ -76,10 +119,10 @@ int main(int argc, char **argv) {
     const int cus = prop.multiProcessorCount;
     unsigned *count, *fail;
     float *buf;
-    CK(hipMalloc(&count, 8));
+    CK(hipMalloc(&count, 2048));
     CK(hipMalloc(&fail, 4));
     CK(hipMalloc(&buf, (size_t)64 << 20));
-    CK(hipMemset(count, 0, 8));
+    CK(hipMemset(count, 0, 2048));
     CK(hipMemset(fail, 0, 4));
     CK(hipMemset(buf, 0, (size_t)64 << 20));
     hipStream_t st;
@@ -104,6 +147,22 @@ int main(int argc, char **argv) {
             CK(hipMemcpy(&hf, fail, 4, hipMemcpyDeviceToHost));
             std::printf("barrier    G %4d: %7.3f us per grid barrier (%d barriers in one launch)%s\n", G,
                         ms * 1e3 / n, n, hf ? "  SPIN BOUND HIT" : "");
+            if (hf) return 2;
+        }
+        for (int rep = 0; rep < 2; ++rep) {
+            const int n = 2000;
+            unsigned *c2 = count + 64;   // its own lines, past the flat barrier's words
+            k_barriers2<<<G, 256, 0, st>>>(c2, (unsigned)G, 10, fail);   // warm
+            CK(hipEventRecord(a, st));
+            k_barriers2<<<G, 256, 0, st>>>(c2, (unsigned)G, n, fail);
+            CK(hipEventRecord(b, st));
+            CK(hipEventSynchronize(b));
+            float ms = 0;
+            CK(hipEventElapsedTime(&ms, a, b));
+            unsigned hf = 0;
+            CK(hipMemcpy(&hf, fail, 4, hipMemcpyDeviceToHost));
+            std::printf("barrier2   G %4d: %7.3f us per grid barrier (two-level: 8 groups, then global)%s\n", G,
+                        ms * 1e3 / n, hf ? "  SPIN BOUND HIT" : "");
             if (hf) return 2;
         }
         for (int rep = 0; rep < 2; ++rep) {
