@@ -382,6 +382,32 @@ def rank_fail(msg):
     os._exit(3)
 
 
+def host_cpus():
+    """CPUs this process may use: its affinity mask and the cgroup v2 quota"""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()
+            if q != "max":
+                n = min(n, max(1, int(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+# host cores one rank keeps busy (profiles/r06/host_sync): ~1.9 with the HIP runtime
+# spinning on its waits, ~1.1 with the waits sleeping (SPAI_BLOCKING_SYNC, -0.3 % sims/s)
+SPIN_CORES_PER_RANK = 2.0
+
+
+def host_sync_mode(local_world, cpus):
+    """spin-wait on the device (the faster default) unless the ranks on this node would
+    then need more host cores than the process may use; an explicit SPAI_BLOCKING_SYNC wins"""
+    if "SPAI_BLOCKING_SYNC" in os.environ:
+        return "blocking" if os.environ["SPAI_BLOCKING_SYNC"] not in ("", "0") else "spin"
+    return "blocking" if SPIN_CORES_PER_RANK * local_world > cpus else "spin"
+
+
 def stream_base(first, k, world, rank, G):
     """first game id of rank `rank`'s stream of k steps' games starting at step
     `first`: the ranks' ranges [(first * world + rank * k) * G, + k * G) tile
@@ -402,6 +428,14 @@ def main():
         sys.exit("bench.py: --gpus %d but the launcher started WORLD_SIZE=%s ranks"
                  % (args.gpus, os.environ["WORLD_SIZE"]))
     dist = Dist()
+    # the host-core budget of a node's ranks: each rank's host loop spins on
+    # its device waits (~1.9 cores); when the ranks of this node would need more cores than
+    # the process may use, the waits sleep instead (~1.1 cores).  Set before the first
+    # device use in this process, which is when the library reads it.
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", dist.world))
+    cpus = host_cpus()
+    sync_mode = host_sync_mode(local_world, cpus)
+    os.environ["SPAI_BLOCKING_SYNC"] = "1" if sync_mode == "blocking" else "0"
     import spai
 
     eng = spai.Engine(num_searches=args.sims, max_trees=args.games, eval_kind=spai.EVAL_NET, device=dist.local,
@@ -546,8 +580,11 @@ def main():
                  "cores_per_node_at_8_ranks": 8 * max(r["host_cpu_share"] for r in per_rank),
                  "sims_per_sec_rank_spread": (max(r["sims_per_sec"] for r in per_rank) /
                                               min(r["sims_per_sec"] for r in per_rank)),
+                 "sync": sync_mode, "cpus_available": cpus, "ranks_on_node": local_world,
                  "note": "host CPU seconds (getrusage of each rank process: user + system, all threads) over the "
-                         "timed region; share = CPU seconds / the rank's own wall time, i.e. host cores busy per GPU"},
+                         "timed region; share = CPU seconds / the rank's own wall time, i.e. host cores busy per GPU; "
+                         "sync = how the ranks wait on their devices (spin, or sleep when %g cores x ranks exceed "
+                         "the CPUs the process may use)" % SPIN_CORES_PER_RANK},
         "evals_per_sec": evals / dt_max,
         "positions_per_sec": positions / dt_max,
         "kernel_ms": {k: v["avg_ms"] for k, v in timing.items()},

@@ -190,3 +190,21 @@ def test_rccl_failure_stops_the_rank(tmp_path, world):
     else:
         assert p.returncode == 3 and "returned" not in p.stdout, (p.returncode, p.stdout)
         assert "RCCL communicator failed on rank 0" in p.stderr
+
+
+def test_host_sync_mode(monkeypatch):
+    """the ranks of a node spin on their device waits unless that would need more host
+    cores than the process may use (~2 per spinning rank, profiles/r06/host_sync);
+    SPAI_BLOCKING_SYNC set by the user wins"""
+    sys.path.insert(0, REPO)
+    import bench
+    monkeypatch.delenv("SPAI_BLOCKING_SYNC", raising=False)
+    assert bench.host_sync_mode(1, 16) == "spin"
+    assert bench.host_sync_mode(8, 16) == "spin"
+    assert bench.host_sync_mode(8, 12) == "blocking"
+    assert bench.host_sync_mode(8, 256) == "spin"
+    monkeypatch.setenv("SPAI_BLOCKING_SYNC", "1")
+    assert bench.host_sync_mode(1, 256) == "blocking"
+    monkeypatch.setenv("SPAI_BLOCKING_SYNC", "0")
+    assert bench.host_sync_mode(8, 4) == "spin"
+    assert bench.host_cpus() >= 1
