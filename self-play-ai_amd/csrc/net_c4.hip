@@ -493,7 +493,11 @@ __global__ __launch_bounds__(64) void k_geo_init(const uint4 *__restrict__ geo, 
 #define SPAI_DB4 2   // B ring at S = 4 (tuning knob)
 #endif
 #ifndef SPAI_DA8
+#ifdef SPAI_FINAL2
+#define SPAI_DA8 6   // the two-tap final phase (final_phase2) holds k-steps 14-17 in four ring slots
+#else
 #define SPAI_DA8 3   // A ring at S >= 5 (tuning knob)
+#endif
 #endif
 #ifndef SPAI_DB8
 #define SPAI_DB8 2   // B ring at S >= 5 (tuning knob)
@@ -620,6 +624,25 @@ __device__ __forceinline__ void final_tap_epilogue(uint8_t *smem, const Geo<Plan
             nw = 1;
 #endif
             nv = 0;
+#elif defined(SPAI_EXP_STORE_B128)
+            // timing-only experiment (wrong results): the same bytes as half as many 16-B
+            // stores (task pairs; the second task of a pair stores nothing)
+            if ((j & 1) == 0) {
+                const uint32_t a0 = pack_relu_bf16x2(acc[j][0], acc[j][1]), a1 = pack_relu_bf16x2(acc[j][2], acc[j][3]);
+                const int j2 = j + 1 < PL::n ? j + 1 : j;
+                const uint32_t b0 = pack_relu_bf16x2(acc[j2][0], acc[j2][1]), b1 = pack_relu_bf16x2(acc[j2][2], acc[j2][3]);
+                *(uint4 *)(smem + (off & ~15)) = make_uint4(a0, a1, b0, b1);
+                nw = 1;
+            }
+            nv = 5;
+#elif defined(SPAI_EXP_STORE_LIN)
+            // timing-only experiment (wrong results): the same stores at bank-conflict-free
+            // addresses (each 16-lane group writes 128 contiguous bytes)
+            (void)off;
+            *(uint2 *)(smem + OUT + j * 512 + lane * 8) = make_uint2(pack_relu_bf16x2(acc[j][0], acc[j][1]),
+                                                                     pack_relu_bf16x2(acc[j][2], acc[j][3]));
+            nv = 5;
+            nw = 1;
 #else
             *(uint2 *)(smem + off) = make_uint2(pack_relu_bf16x2(acc[j][0], acc[j][1]), pack_relu_bf16x2(acc[j][2], acc[j][3]));
             nv = 5;
@@ -659,6 +682,106 @@ __device__ __forceinline__ void final_tap_epilogue(uint8_t *smem, const Geo<Plan
 #pragma unroll
         for (int i = 0; i < PL::n; ++i)
             if (PL::deferred(i)) dacc[i] = acc[i];
+    }
+}
+
+// SPAI_FINAL2: at the position-major group sizes (S >= 5) the last TWO taps (k-steps
+// 14-17) run task-major with the epilogue fused, so the LDS stores of the finished
+// tasks overlap twice as many MFMAs as in final_tap_epilogue (round 6: a trunk conv's
+// ~750 cycles of epilogue stores otherwise outlast its last tap, profiles/r06).  Each
+// task still adds its k-steps in order, so the results are those of the default.  The
+// B fragments of k-steps 14-17 are read per position tile, one tile ahead; the weights
+// of k-steps 14-17 sit in four distinct slots of the A ring (DA = 6).
+#ifdef SPAI_FINAL2
+constexpr bool kFinal2 = true;
+#else
+constexpr bool kFinal2 = false;
+#endif
+template <int W, int CT, int NPT, int S, int IN, int DA, int EPI, int OUT>
+__device__ __forceinline__ void final_phase2(uint8_t *smem, const Geo<Plan<W, CT, NPT>::NT> &g, int lane,
+                                             const uint4 (&A)[DA][Plan<W, CT, NPT>::CTL],
+                                             f32x4 (&acc)[Plan<W, CT, NPT>::n]) {
+    using PL = Plan<W, CT, NPT>;
+    constexpr int n = PL::n, NT = PL::NT, k0 = kKStepsRes - 4, D = 2;
+    static_assert(CT == 4 && PL::MODE == 0 && (EPI == 1 || EPI == 2), "final_phase2: position-major trunk convs");
+    static_assert(DA >= 6, "final_phase2: k-steps 14-17 need four distinct A slots");
+    auto live = [](int t, int ks) { return !((tap_skip(S, PL::gpt(t)) >> (ks >> 1)) & 1); };
+    uint4 Bf[2][4];   // k-steps 14-17 of one local tile, double-buffered over the tiles
+    auto read_tile = [&](int t) {
+        int nr = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int ks = k0 + k, tap = ks >> 1, flip = (ks & 1) << 6;
+            if (live(t, ks)) {
+                Bf[t & 1][k] = *(const uint4 *)(smem + (IN - 256) + (g.b(t, tap) ^ flip));
+                ++nr;
+            }
+        }
+        return nr;
+    };
+    uint4 id[2];   // the residual identities (final_tap_epilogue)
+    uint4 rb[3];   // residual B fragments, two tasks ahead
+    if (EPI == 2) {
+        const int m = lane & 15, q = lane >> 4;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int j = 16 * h + m - 8 * q;
+            uint32_t w[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) w[e] = j == 2 * e ? 0x3F80u : j == 2 * e + 1 ? 0x3F800000u : 0u;
+            id[h] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+#pragma unroll
+        for (int i = 0; i < 2 && i < n; ++i)
+            rb[i] = *(const uint4 *)(smem + (OUT - 256) + (g.b(PL::pt(i), 4) ^ ((PL::co(i) >> 1) << 6)));
+    }
+    read_tile(PL::pt(0));
+#pragma unroll
+    for (int i = 0; i < n + D; ++i) {
+        int nm = 0, nv = 0, nw = 0, nrd = 0;
+        if (i < n) {
+            const int t = PL::pt(i), c = PL::co(i) - PL::C0;
+            if ((i == 0 || PL::pt(i - 1) != t) && t + 1 < NT) nrd += read_tile(t + 1);   // the next tile, one tile ahead
+            if (EPI == 2 && i + 2 < n) {
+                rb[(i + 2) % 3] = *(const uint4 *)(smem + (OUT - 256) + (g.b(PL::pt(i + 2), 4) ^ ((PL::co(i + 2) >> 1) << 6)));
+                ++nrd;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (live(t, k0 + k)) {   // (the bias went in with the first live k-step, <= 8)
+                    acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(A[(k0 + k) % DA][c]),
+                                                                    as_bf16x8(Bf[t & 1][k]), acc[i], 0, 0, 0);
+                    ++nm;
+                }
+            if (EPI == 2) {
+                acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(id[PL::co(i) & 1]), as_bf16x8(rb[i % 3]), acc[i],
+                                                                0, 0, 0);
+                ++nm;
+            }
+        }
+        if (i >= D) {
+            const int j = i - D;
+            const int off = OUT + (g.epi[PL::pt(j)] ^ (PL::co(j) << 5));
+            *(uint2 *)(smem + off) = make_uint2(pack_relu_bf16x2(acc[j][0], acc[j][1]), pack_relu_bf16x2(acc[j][2], acc[j][3]));
+            nv = 9;
+            nw = 1;
+        }
+        // issue order: each MFMA followed by 2 of the epilogue's VALU, then the rest, the
+        // store and the reads
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            if (k < nm) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (nv) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+            }
+        if (nv && nm < 5) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        if (nv && nm < 4) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        if (nv && nm < 3) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        if (nw) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            if (k < nrd) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -725,9 +848,25 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
             for (int c = 0; c < CTL; ++c) A[(ks + la) % DA][c] = exp_a(wnl[((ks + la - kKStepsRes) * CT + c) * 64], lane, ks + c);
         }
     };
+    // k-steps in the task-major final phase: 4 with SPAI_FINAL2 at the position-major sizes
+    constexpr int KF = (EPI == 1 || EPI == 2) && kFinal2 && PL::MODE == 0 ? 4 : 2;
+    constexpr int kBEnd = KF == 2 ? kKStepsRes : kKStepsRes - KF;   // the ring's B reads end here
 #pragma unroll
     for (int ks = 0; ks < kKStepsRes; ++ks) {
-        if constexpr (EPI > 0) if (ks == kKStepsRes - 2) {
+        if constexpr (KF == 4) if (ks == kKStepsRes - 4) {
+            // the next layer's second k-step's weights go to the slot k-step 13 left; the
+            // slots of k-steps 14-16 refill after the final phase
+            load_a(ks);
+            final_phase2<W, CT, NPT, S, IN, DA, EPI, OUT>(smem, g, lane, A, acc);
+            load_a(ks + 1);
+            load_a(ks + 2);
+            load_a(ks + 3);
+#ifdef SPAI_DIAG_KSTEP
+            if (kst) kst[ks] = __builtin_amdgcn_s_memtime();
+#endif
+            break;
+        }
+        if constexpr (EPI > 0 && KF == 2) if (ks == kKStepsRes - 2) {
             // B reads of the last k-step (if not issued yet), then the fused final tap;
             // k-step 17's A prefetch waits for the MFMAs that read the slot it refills
             if (ks + lb < kKStepsRes) {
@@ -746,7 +885,7 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
         }
         load_a(ks);
         int nr = 0;   // B reads issued this k-step (for the issue-order hints)
-        if (ks + lb < kKStepsRes) {
+        if (ks + lb < kBEnd) {
             const int tap = (ks + lb) >> 1, flip = ((ks + lb) & 1) << 6;
 #pragma unroll
             for (int t = 0; t < NT; ++t)
