@@ -358,28 +358,29 @@ class _StdoutToStderr:
 
 def rccl_comm(dist, spai):
     """an RCCL communicator over the ranks' devices (rank 0's id through the host
-    group); None with a reason when the ranks share a device (RCCL refuses that)"""
+    group); None with a reason when the ranks share a device (RCCL refuses that) or
+    when it could not be formed on every rank.  spai_comm_create is non-blocking with
+    a bounded wait (SPAI_COMM_TIMEOUT_S), so a rank whose peer failed gets an error
+    back instead of hanging in ncclCommInitRank; the ranks then agree over the host
+    group, and without a communicator on every rank none uses one (the host group
+    carries the reductions either way)."""
     devs = dist.g.allgather(dist.local)
     if len(set(devs)) != len(devs):
         return None, "ranks share device(s) %s: RCCL needs one rank per GPU; host group only" % devs
+    comm, err = None, None
     try:
         with _StdoutToStderr():
             uid = dist.g.broadcast_bytes(spai.comm_unique_id() if dist.rank == 0 else None)
             comm = spai.Comm(dist.local, dist.rank, dist.world, uid)
     except Exception as ex:
-        if dist.world > 1:   # the peers may be blocked inside ncclCommInitRank (no timeout): exit so the
-            rank_fail("RCCL communicator failed on rank %d: %r" % (dist.rank, ex))   # launcher stops them
-        return None, "RCCL communicator failed: %r" % (ex,)   # 1 rank: reported in the line
-    if dist.world > 1 and not all(dist.g.allgather(True)):   # every rank formed it before any collective
-        rank_fail("RCCL communicator: not every rank formed it")
+        err = "rank %d: %r" % (dist.rank, ex)
+    errs = [e for e in dist.g.allgather(err)] if dist.world > 1 else [err]
+    if any(errs):
+        if comm is not None:
+            with _StdoutToStderr():
+                comm.close()
+        return None, "RCCL communicator failed (%s); host group only" % "; ".join(e for e in errs if e)
     return comm, None
-
-
-def rank_fail(msg):
-    """a rank of an N > 1 run that cannot go on: exit non-zero at once, so spawn_ranks (or
-    the launcher) stops the other ranks instead of leaving them in an RCCL collective"""
-    print("bench.py: " + msg, file=sys.stderr, flush=True)
-    os._exit(3)
 
 
 def host_cpus():
@@ -497,18 +498,19 @@ def main():
     sims, games, evals, positions = dist.reduce(counters, "sum")
     rccl = {"ranks": 0, "note": comm_note}
     if comm is not None:   # the same reductions over RCCL (xGMI between GPUs): exact for these integer counts
+        r_sum = r_max = err = None
         try:
             with _StdoutToStderr():
                 r_sum = comm.allreduce(counters, "sum")
                 (r_max,) = comm.allreduce([dt], "max")
+        except Exception as ex:   # bounded inside the library: a failed or absent peer returns an error
+            err = "rank %d: %r" % (dist.rank, ex)
+        errs = dist.g.allgather(err) if dist.world > 1 else [err]
+        if any(errs):
+            rccl = {"ranks": 0, "note": "RCCL all-reduce failed (%s); host group only" % "; ".join(e for e in errs if e)}
+        else:
             rccl = {"ranks": comm.info()[1], "devices": dist.g.allgather(dist.local),
                     "counters_agree": r_sum == [sims, games, evals, positions] and r_max == dt_max}
-        except Exception as ex:
-            if dist.world > 1:
-                rank_fail("RCCL all-reduce failed on rank %d: %r" % (dist.rank, ex))
-            rccl = {"ranks": 0, "note": "RCCL all-reduce failed: %r" % (ex,)}
-        if dist.world > 1 and not all(dist.g.allgather(True)):
-            rank_fail("RCCL all-reduce: not every rank completed it")
         with _StdoutToStderr():
             comm.close()
 

@@ -13,7 +13,22 @@
 #include <rccl/rccl.h>
 #include <string.h>
 
+#include <chrono>
+#include <cstdlib>
+#include <thread>
+
 #include "spai_internal.h"
+
+// Every RCCL call here is non-blocking (ncclConfig_t.blocking = 0) and waited for
+// with a bound (SPAI_COMM_TIMEOUT_S, default 120 s): a rank whose peer failed or never
+// arrived gets SPAI_ERR_DEVICE back (the communicator aborted) instead of blocking
+// forever inside ncclCommInitRank or a collective, so the caller can agree with the
+// other ranks over its host group and go on without RCCL.
+static double comm_timeout_s() {
+    const char *v = std::getenv("SPAI_COMM_TIMEOUT_S");
+    const double t = v ? std::atof(v) : 120.0;
+    return t > 0 ? t : 120.0;
+}
 
 struct spai_comm {
     int device = 0;
@@ -24,6 +39,19 @@ struct spai_comm {
 };
 
 namespace spai {
+
+// wait (bounded) until the communicator's pending operation leaves ncclInProgress
+static ncclResult_t comm_wait(ncclComm_t comm, double seconds) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t r = ncclCommGetAsyncError(comm, &st);
+        if (r != ncclSuccess) return r;
+        if (st != ncclInProgress) return st;
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > seconds) return ncclInProgress;
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
 
 void comm_destroy(spai_comm *c) {
     if (!c) return;
@@ -56,11 +84,15 @@ int comm_create(int device, int rank, int world, const uint8_t *id, spai_comm **
     ncclUniqueId uid;
     static_assert(sizeof(uid.internal) == SPAI_COMM_ID_BYTES, "RCCL unique id size");
     memcpy(uid.internal, id, SPAI_COMM_ID_BYTES);
-    const ncclResult_t r = ncclCommInitRank(&c->comm, world, uid, rank);
+    ncclConfig_t config = NCCL_CONFIG_INITIALIZER;
+    config.blocking = 0;
+    ncclResult_t r = ncclCommInitRankConfig(&c->comm, world, uid, rank, &config);
+    if (r == ncclInProgress || (r == ncclSuccess && c->comm)) r = comm_wait(c->comm, comm_timeout_s());
     if (r != ncclSuccess) {
+        if (c->comm) (void)ncclCommAbort(c->comm);
         c->comm = nullptr;
         set_error("ncclCommInitRank(world %d, rank %d, device %d) failed: %s", world, rank, device,
-                  ncclGetErrorString(r));
+                  r == ncclInProgress ? "timed out (a peer failed or never arrived)" : ncclGetErrorString(r));
         return fail(SPAI_ERR_DEVICE);
     }
     int nr = 0;
@@ -77,14 +109,32 @@ int comm_create(int device, int rank, int world, const uint8_t *id, spai_comm **
 int comm_allreduce_f64(spai_comm *c, double *host, size_t n, int op) {
     SPAI_CHECK(op == SPAI_REDUCE_SUM || op == SPAI_REDUCE_MAX, SPAI_ERR_INVALID, "reduce op %d", op);
     if (n == 0) return SPAI_OK;
+    SPAI_CHECK(c->comm, SPAI_ERR_DEVICE, "the communicator was aborted by an earlier failure");
     SPAI_HIP(hipSetDevice(c->device));
     if (c->buf.n < n) SPAI_TRY(c->buf.alloc(n));
     SPAI_HIP(hipMemcpyAsync(c->buf.p, host, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    const ncclResult_t r = ncclAllReduce(c->buf.p, c->buf.p, n, ncclFloat64, op == SPAI_REDUCE_SUM ? ncclSum : ncclMax,
-                                         c->comm, c->stream);
-    SPAI_CHECK(r == ncclSuccess, SPAI_ERR_DEVICE, "ncclAllReduce of %zu doubles failed: %s", n, ncclGetErrorString(r));
+    ncclResult_t r = ncclAllReduce(c->buf.p, c->buf.p, n, ncclFloat64, op == SPAI_REDUCE_SUM ? ncclSum : ncclMax,
+                                   c->comm, c->stream);
+    if (r == ncclInProgress) r = comm_wait(c->comm, comm_timeout_s());
     SPAI_HIP(hipMemcpyAsync(host, c->buf.p, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    SPAI_HIP(hipStreamSynchronize(c->stream));
+    // the collective runs on the stream: wait for it with the same bound
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t q = hipErrorNotReady;
+    while (r == ncclSuccess && (q = hipStreamQuery(c->stream)) == hipErrorNotReady) {
+        ncclResult_t st = ncclSuccess;
+        if (ncclCommGetAsyncError(c->comm, &st) != ncclSuccess || (st != ncclSuccess && st != ncclInProgress)) r = st;
+        else if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > comm_timeout_s())
+            r = ncclInProgress;
+        else std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    if (r != ncclSuccess) {   // abort: the stream's collective can then return; the communicator is unusable
+        (void)ncclCommAbort(c->comm);
+        c->comm = nullptr;
+        set_error("ncclAllReduce of %zu doubles failed: %s", n,
+                  r == ncclInProgress ? "timed out (a peer failed or never arrived)" : ncclGetErrorString(r));
+        return SPAI_ERR_DEVICE;
+    }
+    SPAI_CHECK(q == hipSuccess, SPAI_ERR_DEVICE, "comm stream: %s", hipGetErrorString(q));
     return SPAI_OK;
 }
 
