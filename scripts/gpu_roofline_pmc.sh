@@ -7,6 +7,9 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 TAG=${TAG:-rpmc}; O=gpurun_out/$TAG; mkdir -p $O
+# a pass prints nothing for minutes: keep gpurun's silence watchdog informed
+( while sleep 50; do date >> $O/heartbeat.txt; done ) & HB=$!
+trap "kill $HB 2>/dev/null" EXIT
 BA="--warmup 0 --no-cpu-baseline --no-isolated --no-rules-bench --no-chess --no-lockstep-ref ${BENCH_ARGS:-}"
 # the traffic passes over one streamed step; the SQ pass over SQ_STEPS (default 2), so its
 # mix of group sizes (and so executed / algorithmic MFMA FLOPs) is nearer the default run's
