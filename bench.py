@@ -403,10 +403,12 @@ SPIN_CORES_PER_RANK = 2.0
 
 def host_sync_mode(local_world, cpus):
     """spin-wait on the device (the faster default) unless the ranks on this node would
-    then need more host cores than the process may use; an explicit SPAI_BLOCKING_SYNC wins"""
+    then keep more than 3/4 of the host cores the process may use busy (the rest is
+    headroom for the HIP runtime's threads and the host group); an explicit
+    SPAI_BLOCKING_SYNC wins"""
     if "SPAI_BLOCKING_SYNC" in os.environ:
         return "blocking" if os.environ["SPAI_BLOCKING_SYNC"] not in ("", "0") else "spin"
-    return "blocking" if SPIN_CORES_PER_RANK * local_world > cpus else "spin"
+    return "blocking" if SPIN_CORES_PER_RANK * local_world > 0.75 * cpus else "spin"
 
 
 def stream_base(first, k, world, rank, G):
@@ -586,7 +588,7 @@ def main():
                  "note": "host CPU seconds (getrusage of each rank process: user + system, all threads) over the "
                          "timed region; share = CPU seconds / the rank's own wall time, i.e. host cores busy per GPU; "
                          "sync = how the ranks wait on their devices (spin, or sleep when %g cores x ranks exceed "
-                         "the CPUs the process may use)" % SPIN_CORES_PER_RANK},
+                         "3/4 of the CPUs the process may use)" % SPIN_CORES_PER_RANK},
         "evals_per_sec": evals / dt_max,
         "positions_per_sec": positions / dt_max,
         "kernel_ms": {k: v["avg_ms"] for k, v in timing.items()},
