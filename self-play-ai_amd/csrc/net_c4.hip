@@ -415,7 +415,10 @@ __device__ __forceinline__ void make_geo(const uint8_t *smem, int lane, Geo<Plan
 // (S, W, t) of the 64-channel layers' plan (the head conv runs on it too) holds
 // 64 lanes x 32 B: {rel2[5], epi, aux, 0}; aux = s | (bit col*7+row) << 8 for the
 // stem and the head-feature offsets (padding rows: s = S, a zeroed plane row).
-constexpr int kGeoNT = 8;   // the most position tiles a wave holds (S = 3, co-major)
+#ifndef SPAI_GEO_NT
+#define SPAI_GEO_NT 8
+#endif
+constexpr int kGeoNT = SPAI_GEO_NT;   // the most position tiles a wave holds (S = 3, co-major; 11 for a pair split at S = 8)
 __host__ __device__ constexpr size_t lane_geo_at(int S, int W, int t) {
     return (((size_t)(S - 1) * kWaves + W) * kGeoNT + t) * 64 * 2;   // in uint4
 }
