@@ -489,6 +489,14 @@ __global__ __launch_bounds__(64) void k_geo_init(const uint4 *__restrict__ geo, 
 // hide a weight load (L2) or an LDS read behind, but registers to spare.
 // (DA must divide the 18 k-steps of a layer: the ring carries the next layer's
 // first DA-1 k-steps in the slots a fresh layer expects.)
+// scheduling of an ordinary k-step (knobs, round 6): the MFMA / VALU / LDS / VMEM
+// interleave hints, and the scheduling fence that closes each k-step
+#ifndef SPAI_ISSUE_HINTS
+#define SPAI_ISSUE_HINTS 0   // 1: the round-3 interleave hints (-2.5 % sims/s in round 6, profiles/r06/sched)
+#endif
+#ifndef SPAI_KSTEP_FENCE
+#define SPAI_KSTEP_FENCE 1
+#endif
 #ifndef SPAI_DA4
 #define SPAI_DA4 6   // A ring at S = 4 (tuning knob)
 #endif
@@ -503,7 +511,7 @@ __global__ __launch_bounds__(64) void k_geo_init(const uint4 *__restrict__ geo, 
 #endif
 #endif
 #ifndef SPAI_DB8
-#define SPAI_DB8 2   // B ring at S >= 5 (tuning knob)
+#define SPAI_DB8 3   // B ring at S >= 5 (tuning knob; 3 since round 6 without the issue hints: +0.5 %, profiles/r06/sched)
 #endif
 __host__ __device__ constexpr int a_depth(int S) { return S <= 2 ? 9 : S <= 3 ? 6 : S <= 4 ? SPAI_DA4 : SPAI_DA8; }
 __host__ __device__ constexpr int b_depth(int S) { return S <= 2 ? 4 : S <= 3 ? 3 : S <= 4 ? SPAI_DB4 : SPAI_DB8; }
@@ -911,6 +919,7 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
         // issue order for this k-step: each MFMA followed by up to 2 VALU, one
         // LDS read (next B) and one weight load (A, DA-1 ahead)
         const int ng = nm > nr ? nm : nr;
+#if SPAI_ISSUE_HINTS
 #pragma unroll
         for (int i = 0; i < PL::n; ++i) {
             if (i < ng) {
@@ -920,7 +929,12 @@ __device__ __forceinline__ void conv_mfma(uint8_t *smem, const Geo<Plan<W, CT, N
                 if (i < CTL) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
             }
         }
+#else
+        (void)ng;
+#endif
+#if SPAI_KSTEP_FENCE
         __builtin_amdgcn_sched_barrier(0);
+#endif
 #ifdef SPAI_DIAG_KSTEP
         if (kst) kst[ks] = __builtin_amdgcn_s_memtime();
 #endif
