@@ -100,7 +100,7 @@ def parse():
     ap.add_argument("--no-isolated", action="store_true", help="skip the isolated-forward measurement")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r05", "final", "forward_traffic.json"),
                     help="PMC summary (scripts/gpu_traffic.sh) of this bench command: HBM bytes per k_forward launch")
-    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r06", "final_s2", "forward_pmc.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "r06", "final_s3", "forward_pmc.json"),
                     help="PMC summary of this bench command (scripts/gpu_roofline_pmc.sh): executed MFMA FLOPs, MFMA "
                          "busy cycles and HBM bytes per k_forward launch; preferred over --traffic-json when present")
     ap.add_argument("--chess-cpu-seconds", type=float, default=15.0,
