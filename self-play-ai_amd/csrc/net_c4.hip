@@ -491,6 +491,13 @@ __global__ __launch_bounds__(64) void k_geo_init(const uint4 *__restrict__ geo, 
 // first DA-1 k-steps in the slots a fresh layer expects.)
 // scheduling of an ordinary k-step (knobs, round 6): the MFMA / VALU / LDS / VMEM
 // interleave hints, and the scheduling fence that closes each k-step
+// the fused last tap's per-task hints and fence (final_tap_epilogue; knobs)
+#ifndef SPAI_FINAL_HINTS
+#define SPAI_FINAL_HINTS 1
+#endif
+#ifndef SPAI_FINAL_FENCE
+#define SPAI_FINAL_FENCE 1
+#endif
 #ifndef SPAI_ISSUE_HINTS
 #define SPAI_ISSUE_HINTS 0   // 1: the round-3 interleave hints (-2.5 % sims/s in round 6, profiles/r06/sched)
 #endif
@@ -668,6 +675,7 @@ __device__ __forceinline__ void final_tap_epilogue(uint8_t *smem, const Geo<Plan
             nw = 1;
         }
         // issue order: the MFMAs with the epilogue's 5 VALU in their gaps, then the store and the read
+#if SPAI_FINAL_HINTS
         if (nm >= 1) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             if (nv) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
@@ -687,7 +695,14 @@ __device__ __forceinline__ void final_tap_epilogue(uint8_t *smem, const Geo<Plan
         }
         if (nw) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
         if (nrd) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#else
+        (void)nv;
+        (void)nw;
+        (void)nrd;
+#endif
+#if SPAI_FINAL_FENCE
         __builtin_amdgcn_sched_barrier(0);
+#endif
     }
     if constexpr (EPI < 3 && PL::ND > 0) {
 #pragma unroll
