@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT && export TMPDIR=/tmp && O=gpurun_out/${TAG:-sched3} && mkdi
 ( while sleep 50; do date >> $O/heartbeat.txt; done ) & HB=$!
 trap "kill $HB 2>/dev/null" EXIT
 ARGS="--no-cpu-baseline --no-rules-bench --no-chess"
-for i in 1 2; do
+for i in ${REPS:-1 2}; do
   for v in new fh0 fh0ff0 db4; do
     if [ $v = new ]; then L=self-play-ai_amd/libspai.so; else L=ablibs/libspai_$v.so; fi
     SPAI_LIB=$L timeout -k 10 300 python3 bench.py $ARGS > $O/${v}_$i.json 2> $O/${v}_$i.err || { tail -5 $O/${v}_$i.err; exit 1; }
